@@ -1,0 +1,117 @@
+"""Headline benchmark: training tokens/sec of the bundled Llama-3-8B PyTorch-ROCm chart on N MI355X.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 launched by torchrun,
+one rank per GPU over RCCL. W untimed warmup steps, then EXACTLY K timed optimizer steps bracketed by a
+barrier + device synchronize on both sides; the MAX step time over ranks is used; rank 0 prints one JSON
+line. ``value`` is the whole-job throughput (sum over ranks = N x per-rank tokens / max time).
+
+Every timed step is a complete training step: forward through all 32 layers, cross-entropy over the full
+128,256 vocabulary, backward, bucketed RCCL gradient collectives (N > 1), gradient clipping and the fused
+AdamW update of all 8.03 B parameters. Weights are random-init, tokens synthetic (no network / datasets).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="llama3_8b")
+    ap.add_argument("--seq", type=int, default=8192)
+    ap.add_argument("--mbs", type=int, default=1, help="micro-batch (sequences) per rank")
+    ap.add_argument("--accum", type=int, default=1, help="gradient-accumulation micro-batches per step")
+    ap.add_argument("--dp", default="allreduce", choices=["allreduce", "zero1"])
+    ap.add_argument("--bucket-mb", type=int, default=512)
+    ap.add_argument("--device", default="auto")
+    args = ap.parse_args()
+
+    import torch
+
+    from kubeoperator_amd.parallel.dist import all_reduce_max, barrier, init_distributed, shutdown
+    from kubeoperator_amd.train import SyntheticTokens, TrainConfig, Trainer
+
+    info = init_distributed(args.device)
+    world = info.world
+    if world != args.gpus and info.is_main:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the real world size",
+              file=sys.stderr)
+    tc = TrainConfig(model=args.model, micro_batch=args.mbs, seq_len=args.seq, grad_accum=args.accum,
+                     dp_mode=args.dp, bucket_mb=args.bucket_mb, warmup_steps=10, total_steps=1000)
+    trainer = Trainer(tc, info)
+    data = SyntheticTokens(trainer.cfg.vocab_size, args.mbs, args.seq, info.device, seed=tc.seed, rank=info.rank)
+    cuda = info.device.type == "cuda"
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+
+    loss = None
+    for _ in range(args.warmup):
+        loss = trainer.train_step(data.batches(args.accum))
+    sync()
+    barrier(info)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = trainer.train_step(data.batches(args.accum))
+    sync()
+    barrier(info)
+    sync()
+    elapsed = time.perf_counter() - t0
+    elapsed = all_reduce_max(elapsed, info)
+    last_loss = float(loss.item()) if loss is not None else float("nan")
+    tokens = world * trainer.tokens_per_step * args.steps
+    value = tokens / elapsed
+    ms = elapsed / args.steps * 1000.0
+    cfg = trainer.cfg
+    flops_tok = cfg.flops_per_token(args.seq)
+    mem_gb = torch.cuda.max_memory_allocated() / 1e9 if cuda else 0.0
+    if info.is_main:
+        model_name = {"llama3_8b": "Llama-3-8B", "gpt2_small": "GPT-2-small"}.get(args.model, args.model)
+        out = {
+            "metric": "tokens/sec of bundled Llama-3-8B pod" if args.model == "llama3_8b"
+            else f"tokens/sec of bundled {model_name} pod",
+            "value": round(value, 2),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (random token ids generated on device; random-init weights)",
+            "config": {
+                "model": model_name,
+                "params": cfg.num_params(),
+                "global_batch": args.mbs * args.accum * world,
+                "micro_batch_per_gpu": args.mbs,
+                "grad_accum": args.accum,
+                "seq_len": args.seq,
+                "parallelism": f"dp{world}" + ("-zero1" if args.dp == "zero1" and world > 1 else ""),
+                "optimizer": "fused AdamW (fp32 master/moments), grad clip 1.0",
+            },
+            "tflops_per_gpu": round(flops_tok * value / world / 1e12, 1),
+            "last_loss": round(last_loss, 4),
+            "peak_mem_gb_rank0": round(mem_gb, 1),
+            "setup_s": round(trainer.setup_seconds, 1),
+        }
+        print(json.dumps(out), flush=True)
+    shutdown(info)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

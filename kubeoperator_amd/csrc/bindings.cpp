@@ -1,0 +1,262 @@
+// PyTorch bindings for the kubeoperator_amd gfx950 kernels.
+//
+// Thin adapters only: validate dtype / device / alignment / strides, pick the current HIP stream,
+// call the raw-pointer launcher from kernels.h. Activations are passed as 2-D [tokens, features]
+// views whose rows may be strided (e.g. the Q, K and V column slices of the fused QKV output), so
+// the attention / RoPE paths never copy or transpose.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include "kernels.h"
+
+namespace {
+
+using at::Tensor;
+using kop::bf16_t;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_gpu(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be on the GPU (HIP device)");
+}
+void check_bf16(const Tensor& t, const char* name) {
+  check_gpu(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16");
+}
+void check_f32(const Tensor& t, const char* name) {
+  check_gpu(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
+}
+void check_aligned(const Tensor& t, const char* name) {
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+// 2-D view with unit inner stride, 16-B aligned rows
+void check_rows(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.dim() == 2, name, " must be 2-D [rows, features]");
+  TORCH_CHECK(t.stride(1) == 1, name, " must have a contiguous last dimension");
+  TORCH_CHECK(t.stride(0) % 8 == 0, name, " row stride must be a multiple of 8 elements");
+  check_aligned(t, name);
+}
+bf16_t* bp(const Tensor& t) { return reinterpret_cast<bf16_t*>(t.data_ptr()); }
+const bf16_t* cbp(const c10::optional<Tensor>& t) {
+  return t.has_value() && t->defined() ? reinterpret_cast<const bf16_t*>(t->data_ptr()) : nullptr;
+}
+void rc(int code, const char* what) { TORCH_CHECK(code == 0, what, " failed with code ", code, " (unsupported shape)"); }
+
+// ------------------------------------------------------------------ norms
+std::vector<Tensor> norm_fwd(const Tensor& x, const c10::optional<Tensor>& residual, const Tensor& w,
+                             const c10::optional<Tensor>& b, double eps, bool layernorm) {
+  check_bf16(x, "x");
+  check_bf16(w, "weight");
+  TORCH_CHECK(x.is_contiguous() && w.is_contiguous(), "norm inputs must be contiguous");
+  const int H = (int)x.size(-1);
+  const int rows = (int)(x.numel() / H);
+  auto y = at::empty_like(x);
+  Tensor s;
+  if (residual.has_value()) {
+    check_bf16(*residual, "residual");
+    TORCH_CHECK(residual->is_contiguous() && residual->sizes() == x.sizes(), "residual shape");
+    s = at::empty_like(x);
+  }
+  auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
+  Tensor mean;
+  if (layernorm) {
+    TORCH_CHECK(b.has_value(), "layernorm needs a bias");
+    check_bf16(*b, "bias");
+    mean = at::empty({rows}, x.options().dtype(at::kFloat));
+  }
+  rc(kop::norm_fwd(bp(x), cbp(residual), bp(w), cbp(b), bp(y), s.defined() ? bp(s) : nullptr, rstd.data_ptr<float>(),
+                   layernorm ? mean.data_ptr<float>() : nullptr, rows, H, (float)eps, layernorm, cur_stream()),
+     "norm_fwd");
+  return {y, s, rstd, mean};
+}
+
+Tensor norm_bwd(const Tensor& dy, const Tensor& s, const Tensor& w, const Tensor& rstd,
+                const c10::optional<Tensor>& mean, const c10::optional<Tensor>& dres, const Tensor& dw,
+                const c10::optional<Tensor>& db, bool layernorm, bool accumulate) {
+  check_bf16(dy, "dy");
+  check_bf16(s, "s");
+  check_bf16(dw, "dw");
+  TORCH_CHECK(dy.is_contiguous() && s.is_contiguous() && dw.is_contiguous(), "norm_bwd inputs must be contiguous");
+  const int H = (int)s.size(-1);
+  const int rows = (int)(s.numel() / H);
+  auto dx = at::empty_like(s);
+  const int parts = kop::norm_bwd_partial_rows(rows);
+  auto part = at::empty({(layernorm ? 2 : 1) * (int64_t)parts * H}, s.options().dtype(at::kFloat));
+  rc(kop::norm_bwd(bp(dy), bp(s), bp(w), rstd.data_ptr<float>(),
+                   mean.has_value() && mean->defined() ? mean->data_ptr<float>() : nullptr, cbp(dres), bp(dx),
+                   part.data_ptr<float>(), bp(dw), db.has_value() ? bp(*db) : nullptr, rows, H, layernorm,
+                   accumulate ? 1 : 0, cur_stream()),
+     "norm_bwd");
+  return dx;
+}
+
+// ------------------------------------------------------------------ elementwise
+void rope_(const Tensor& x, const Tensor& cos_t, const Tensor& sin_t, const c10::optional<Tensor>& pos, int64_t S,
+           int64_t nheads, int64_t D, bool inverse) {
+  check_bf16(x, "x");
+  check_rows(x, "x");
+  check_f32(cos_t, "cos");
+  check_f32(sin_t, "sin");
+  TORCH_CHECK(cos_t.is_contiguous() && sin_t.is_contiguous(), "cos/sin tables must be contiguous");
+  TORCH_CHECK(x.size(1) >= nheads * D, "rope: row narrower than nheads*D");
+  const int* pp = nullptr;
+  if (pos.has_value() && pos->defined()) {
+    TORCH_CHECK(pos->scalar_type() == at::kInt && pos->is_contiguous(), "positions must be contiguous int32");
+    pp = pos->data_ptr<int>();
+  }
+  rc(kop::rope_inplace(bp(x), cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), pp, x.size(0), (int)S, (int)nheads,
+                       (int)D, x.stride(0), inverse, cur_stream()),
+     "rope");
+}
+
+Tensor swiglu_fwd(const Tensor& gu) {
+  check_bf16(gu, "gate_up");
+  TORCH_CHECK(gu.is_contiguous(), "gate_up must be contiguous");
+  const int64_t F = gu.size(-1) / 2;
+  const int64_t T = gu.numel() / (2 * F);
+  auto sizes = gu.sizes().vec();
+  sizes.back() = F;
+  auto h = at::empty(sizes, gu.options());
+  rc(kop::swiglu_fwd(bp(gu), bp(h), T, (int)F, cur_stream()), "swiglu_fwd");
+  return h;
+}
+Tensor swiglu_bwd(const Tensor& gu, const Tensor& dh) {
+  check_bf16(gu, "gate_up");
+  check_bf16(dh, "dh");
+  TORCH_CHECK(gu.is_contiguous() && dh.is_contiguous(), "swiglu_bwd inputs must be contiguous");
+  const int64_t F = gu.size(-1) / 2;
+  const int64_t T = gu.numel() / (2 * F);
+  auto dgu = at::empty_like(gu);
+  rc(kop::swiglu_bwd(bp(gu), bp(dh), bp(dgu), T, (int)F, cur_stream()), "swiglu_bwd");
+  return dgu;
+}
+Tensor gelu_fwd(const Tensor& x) {
+  check_bf16(x, "x");
+  TORCH_CHECK(x.is_contiguous(), "x must be contiguous");
+  auto y = at::empty_like(x);
+  rc(kop::gelu_fwd(bp(x), bp(y), x.numel(), cur_stream()), "gelu_fwd");
+  return y;
+}
+Tensor gelu_bwd(const Tensor& x, const Tensor& dy) {
+  check_bf16(x, "x");
+  check_bf16(dy, "dy");
+  TORCH_CHECK(x.is_contiguous() && dy.is_contiguous(), "gelu_bwd inputs must be contiguous");
+  auto dx = at::empty_like(x);
+  rc(kop::gelu_bwd(bp(x), bp(dy), bp(dx), x.numel(), cur_stream()), "gelu_bwd");
+  return dx;
+}
+
+// ------------------------------------------------------------------ cross entropy
+std::vector<Tensor> cross_entropy_fwd_(const Tensor& logits, const Tensor& targets, int64_t ignore_index,
+                                       bool write_grad, double grad_multiplier) {
+  check_bf16(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be 2-D with a contiguous last dim");
+  TORCH_CHECK(targets.scalar_type() == at::kLong && targets.is_contiguous(), "targets must be contiguous int64");
+  const int64_t T = logits.size(0);
+  TORCH_CHECK(targets.numel() == T, "targets / logits row mismatch");
+  auto f32 = logits.options().dtype(at::kFloat);
+  auto loss = at::empty({T}, f32), lse = at::empty({T}, f32), scale = at::empty({1}, f32);
+  rc(kop::cross_entropy_fwd(bp(logits), logits.stride(0), T, (int)logits.size(1), targets.data_ptr<int64_t>(),
+                            ignore_index, scale.data_ptr<float>(), loss.data_ptr<float>(), lse.data_ptr<float>(),
+                            write_grad, (float)grad_multiplier, cur_stream()),
+     "cross_entropy");
+  return {loss, lse, scale};
+}
+
+// ------------------------------------------------------------------ optimizer
+void adamw_(const Tensor& p, const Tensor& g, const Tensor& master, const Tensor& m, const Tensor& v, double lr,
+            double b1, double b2, double eps, double wd, int64_t step, double gscale,
+            const c10::optional<Tensor>& gscale_dev) {
+  check_bf16(p, "param");
+  check_bf16(g, "grad");
+  check_f32(master, "master");
+  check_f32(m, "exp_avg");
+  check_f32(v, "exp_avg_sq");
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() == n && master.numel() == n && m.numel() == n && v.numel() == n, "adamw size mismatch");
+  for (auto* t : {&p, &g, &master, &m, &v}) {
+    TORCH_CHECK(t->is_contiguous(), "adamw buffers must be contiguous");
+    check_aligned(*t, "adamw buffer");
+  }
+  const float* gd = nullptr;
+  if (gscale_dev.has_value() && gscale_dev->defined()) {
+    check_f32(*gscale_dev, "gscale_dev");
+    gd = gscale_dev->data_ptr<float>();
+  }
+  rc(kop::adamw_step(bp(p), bp(g), master.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), n, (float)lr,
+                     (float)b1, (float)b2, (float)eps, (float)wd, (int)step, (float)gscale, gd, cur_stream()),
+     "adamw");
+}
+void grad_sumsq_(const Tensor& g, const Tensor& out) {
+  check_bf16(g, "grad");
+  check_f32(out, "out");
+  TORCH_CHECK(g.is_contiguous(), "grad must be contiguous");
+  check_aligned(g, "grad");
+  rc(kop::grad_sumsq(bp(g), g.numel(), out.data_ptr<float>(), cur_stream()), "grad_sumsq");
+}
+void clip_coef_(const Tensor& sumsq, double max_norm, const Tensor& coef, const Tensor& norm) {
+  rc(kop::clip_coef(sumsq.data_ptr<float>(), (float)max_norm, coef.data_ptr<float>(), norm.data_ptr<float>(),
+                    cur_stream()),
+     "clip_coef");
+}
+
+// ------------------------------------------------------------------ attention
+void flash_attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& lse, int64_t B,
+                    int64_t S, int64_t Hq, int64_t Hkv, int64_t D, double scale, bool causal) {
+  for (auto* t : {&q, &k, &v, &o}) {
+    check_bf16(*t, "q/k/v/o");
+    check_rows(*t, "q/k/v/o");
+    TORCH_CHECK(t->size(0) == B * S, "attention tensors must have B*S rows");
+  }
+  check_f32(lse, "lse");
+  TORCH_CHECK(lse.numel() == B * Hq * S, "lse size");
+  TORCH_CHECK(q.size(1) >= Hq * D && k.size(1) >= Hkv * D && v.size(1) >= Hkv * D && o.size(1) >= Hq * D,
+              "attention head width");
+  rc(kop::flash_attn_fwd(bp(q), bp(k), bp(v), bp(o), lse.data_ptr<float>(), (int)B, (int)S, (int)Hq, (int)Hkv,
+                         (int)D, q.stride(0), k.stride(0), v.stride(0), o.stride(0), (float)scale, causal,
+                         cur_stream()),
+     "flash_attn_fwd");
+}
+
+int64_t flash_attn_bwd_workspace(int64_t B, int64_t S, int64_t Hq, int64_t D) {
+  return (int64_t)kop::flash_attn_bwd_workspace((int)B, (int)S, (int)Hq, (int)D);
+}
+
+void flash_attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& dout,
+                    const Tensor& lse, const Tensor& dq, const Tensor& dk, const Tensor& dv, const Tensor& workspace,
+                    int64_t B, int64_t S, int64_t Hq, int64_t Hkv, int64_t D, double scale, bool causal) {
+  for (auto* t : {&q, &k, &v, &o, &dout, &dq, &dk, &dv}) {
+    check_bf16(*t, "attention tensor");
+    check_rows(*t, "attention tensor");
+    TORCH_CHECK(t->size(0) == B * S, "attention tensors must have B*S rows");
+  }
+  check_f32(lse, "lse");
+  TORCH_CHECK(workspace.nbytes() >= (size_t)flash_attn_bwd_workspace(B, S, Hq, D), "attention workspace too small");
+  check_aligned(workspace, "workspace");
+  rc(kop::flash_attn_bwd(bp(q), bp(k), bp(v), bp(o), bp(dout), lse.data_ptr<float>(), bp(dq), bp(dk), bp(dv),
+                         workspace.data_ptr(), (int)B, (int)S, (int)Hq, (int)Hkv, (int)D, q.stride(0), k.stride(0),
+                         v.stride(0), o.stride(0), dout.stride(0), dq.stride(0), dk.stride(0), dv.stride(0),
+                         (float)scale, causal, cur_stream()),
+     "flash_attn_bwd");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "kubeoperator_amd gfx950 (MI355X) HIP kernels";
+  m.attr("ARCH") = "gfx950";
+  m.def("norm_fwd", &norm_fwd);
+  m.def("norm_bwd", &norm_bwd);
+  m.def("rope_", &rope_);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("gelu_fwd", &gelu_fwd);
+  m.def("gelu_bwd", &gelu_bwd);
+  m.def("cross_entropy_fwd_", &cross_entropy_fwd_);
+  m.def("adamw_", &adamw_);
+  m.def("grad_sumsq_", &grad_sumsq_);
+  m.def("clip_coef_", &clip_coef_);
+  m.def("flash_attn_fwd", &flash_attn_fwd);
+  m.def("flash_attn_bwd_workspace", &flash_attn_bwd_workspace);
+  m.def("flash_attn_bwd", &flash_attn_bwd);
+}

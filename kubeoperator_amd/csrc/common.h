@@ -1,0 +1,103 @@
+// Shared device helpers for the gfx950 (CDNA4 / MI355X) kernels of kubeoperator_amd.
+//
+// Conventions used by every kernel in this directory:
+//   * wave = 64 lanes; block sizes are multiples of 64;
+//   * bf16 tensors are moved as raw 16-bit patterns in 16-byte vectors (8 x bf16 per lane per load),
+//     converted to fp32 for math, and rounded back with the hardware v_cvt_pk_bf16_f32 (RNE, NaN-safe);
+//   * every launcher is a plain C++ function taking raw device pointers + hipStream_t, so the kernel
+//     translation units compile in seconds without PyTorch headers (bindings.cpp adapts tensors).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+namespace kop {
+
+typedef uint16_t bf16_t;  // raw bf16 bit pattern
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __hip_bfloat16 h = __float2bfloat16(f);
+  return *reinterpret_cast<bf16_t*>(&h);
+}
+
+// pack two floats into one dword of two bf16 (lo in bits 0..15)
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+// 8 x bf16 <-> 8 x f32 for a 16-byte vector
+__device__ __forceinline__ void unpack8(const u32x4 v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(v[i] << 16);
+    f[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ u32x4 pack8(const float* f) {
+  u32x4 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = pack2(f[2 * i], f[2 * i + 1]);
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blocks of NW waves; `red` must hold NW floats of LDS.
+template <int NW>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (NW == 1) return v;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) t += red[i];
+  return t;
+}
+template <int NW>
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (NW == 1) return v;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float t = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) t = fmaxf(t, red[i]);
+  return t;
+}
+
+// Grid size for a memory-bound streaming kernel: enough blocks to fill 256 CUs several times, capped
+// (Guideline 11: grid-stride the rest).
+inline int stream_grid(int64_t work_items, int block) {
+  int64_t g = (work_items + block - 1) / block;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace kop
+
+#define KOP_CHECK_LAUNCH() (void)hipGetLastError()

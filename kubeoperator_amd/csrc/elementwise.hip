@@ -1,0 +1,176 @@
+// Memory-bound elementwise kernels for gfx950: RoPE (in place on the fused QKV activation), SwiGLU and
+// GELU forward/backward. All of them move 16 bytes (8 x bf16) per lane per access (Guideline 13) and
+// take cos/sin from a host-precomputed fp32 table instead of evaluating trig per element (Appendix B).
+#include "common.h"
+#include "kernels.h"
+
+namespace kop {
+
+// ---------------------------------------------------------------------------------------------
+// RoPE, rotate-half convention (x_i, x_{i+D/2}) -> (x_i c - x_{i+D/2} s, x_{i+D/2} c + x_i s),
+// applied in place to the first `nheads` heads of every token row of a [T, row_stride] activation
+// (the Q and K heads of the fused QKV projection; V is untouched). sign = -1 applies the inverse
+// rotation, which is the backward pass. Position of token t is pos[t] if given, else t % S.
+// Work item = 8 consecutive rotary pairs of one head of one token.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) rope_kernel(bf16_t* __restrict__ x, const float* __restrict__ cos_t,
+                                                   const float* __restrict__ sin_t, const int* __restrict__ pos,
+                                                   int64_t T, int S, int nheads, int D, int64_t row_stride,
+                                                   float sign) {
+  const int half = D >> 1;
+  const int per_head = half >> 3;  // work items per head
+  const int64_t total = T * nheads * per_head;
+  for (int it = blockIdx.x * blockDim.x + threadIdx.x; it < (int)total; it += gridDim.x * blockDim.x) {
+    const int j = (int)(it % per_head);
+    const int th = it / per_head;
+    const int h = (int)(th % nheads);
+    const int64_t t = th / nheads;
+    const int p = pos ? pos[t] : (int)(t % S);
+    bf16_t* base = x + t * row_stride + (int64_t)h * D + j * 8;
+    u32x4* lo = reinterpret_cast<u32x4*>(base);
+    u32x4* hi = reinterpret_cast<u32x4*>(base + half);
+    const f32x4* cp = reinterpret_cast<const f32x4*>(cos_t + (int64_t)p * half + j * 8);
+    const f32x4* sp = reinterpret_cast<const f32x4*>(sin_t + (int64_t)p * half + j * 8);
+    float a[8], b[8], c[8], s[8];
+    unpack8(*lo, a);
+    unpack8(*hi, b);
+    f32x4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      c[i] = c0[i];
+      c[i + 4] = c1[i];
+      s[i] = s0[i] * sign;
+      s[i + 4] = s1[i] * sign;
+    }
+    float o1[8], o2[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      o1[i] = a[i] * c[i] - b[i] * s[i];
+      o2[i] = b[i] * c[i] + a[i] * s[i];
+    }
+    *lo = pack8(o1);
+    *hi = pack8(o2);
+  }
+}
+
+int rope_inplace(bf16_t* x, const float* cos_t, const float* sin_t, const int* pos, int64_t T, int S, int nheads,
+                 int D, int64_t row_stride, bool inverse, hipStream_t stream) {
+  if (D % 16 != 0 || row_stride % 8 != 0) return -1;
+  if (T * nheads * (D / 16) >= (1ll << 31)) return -3;
+  const int64_t total = T * nheads * (D / 16);
+  rope_kernel<<<stream_grid(total, 256), 256, 0, stream>>>(x, cos_t, sin_t, pos, T, S, nheads, D, row_stride,
+                                                           inverse ? -1.f : 1.f);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// SwiGLU: gu = [gate | up] along the last dim (one fused GEMM output of width 2F).
+//   fwd: h = silu(gate) * up                  [T, F]
+//   bwd: dgate = dh * up * sig * (1 + gate*(1-sig)),  dup = dh * silu(gate)  -> dgu [T, 2F]
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) swiglu_fwd_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ h,
+                                                         int64_t T, int F) {
+  const int cpr = F >> 3;
+  const int64_t total = T * cpr;
+  for (int it = blockIdx.x * blockDim.x + threadIdx.x; it < (int)total; it += gridDim.x * blockDim.x) {
+    const int64_t t = it / cpr;
+    const int c = (int)(it % cpr);
+    const bf16_t* row = gu + t * 2 * F;
+    float g[8], u[8], o[8];
+    unpack8(reinterpret_cast<const u32x4*>(row)[c], g);
+    unpack8(reinterpret_cast<const u32x4*>(row + F)[c], u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = g[i] / (1.f + __expf(-g[i])) * u[i];
+    reinterpret_cast<u32x4*>(h + t * F)[c] = pack8(o);
+  }
+}
+
+__global__ void __launch_bounds__(256) swiglu_bwd_kernel(const bf16_t* __restrict__ gu, const bf16_t* __restrict__ dh,
+                                                         bf16_t* __restrict__ dgu, int64_t T, int F) {
+  const int cpr = F >> 3;
+  const int64_t total = T * cpr;
+  for (int it = blockIdx.x * blockDim.x + threadIdx.x; it < (int)total; it += gridDim.x * blockDim.x) {
+    const int64_t t = it / cpr;
+    const int c = (int)(it % cpr);
+    const bf16_t* row = gu + t * 2 * F;
+    float g[8], u[8], d[8], dg[8], du[8];
+    unpack8(reinterpret_cast<const u32x4*>(row)[c], g);
+    unpack8(reinterpret_cast<const u32x4*>(row + F)[c], u);
+    unpack8(reinterpret_cast<const u32x4*>(dh + t * F)[c], d);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float sg = 1.f / (1.f + __expf(-g[i]));
+      const float silu = g[i] * sg;
+      du[i] = d[i] * silu;
+      dg[i] = d[i] * u[i] * sg * (1.f + g[i] * (1.f - sg));
+    }
+    bf16_t* orow = dgu + t * 2 * F;
+    reinterpret_cast<u32x4*>(orow)[c] = pack8(dg);
+    reinterpret_cast<u32x4*>(orow + F)[c] = pack8(du);
+  }
+}
+
+int swiglu_fwd(const bf16_t* gu, bf16_t* h, int64_t T, int F, hipStream_t stream) {
+  if (F % 8) return -1;
+  if (T * (F / 8) >= (1ll << 31)) return -3;
+  swiglu_fwd_kernel<<<stream_grid(T * (F / 8), 256), 256, 0, stream>>>(gu, h, T, F);
+  return 0;
+}
+int swiglu_bwd(const bf16_t* gu, const bf16_t* dh, bf16_t* dgu, int64_t T, int F, hipStream_t stream) {
+  if (F % 8) return -1;
+  if (T * (F / 8) >= (1ll << 31)) return -3;
+  swiglu_bwd_kernel<<<stream_grid(T * (F / 8), 256), 256, 0, stream>>>(gu, dh, dgu, T, F);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// GELU (tanh approximation, GPT-2): y = 0.5 x (1 + tanh(k (x + 0.044715 x^3))), k = sqrt(2/pi)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float tanh_fast(float x) {
+  // tanh(x) = 1 - 2/(exp(2x)+1); saturates correctly for large |x|
+  return 1.f - 2.f / (__expf(2.f * x) + 1.f);
+}
+
+__global__ void __launch_bounds__(256) gelu_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int64_t n8) {
+  for (int it = blockIdx.x * blockDim.x + threadIdx.x; it < (int)n8; it += gridDim.x * blockDim.x) {
+    float a[8], o[8];
+    unpack8(reinterpret_cast<const u32x4*>(x)[it], a);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float u = 0.7978845608f * (a[i] + 0.044715f * a[i] * a[i] * a[i]);
+      o[i] = 0.5f * a[i] * (1.f + tanh_fast(u));
+    }
+    reinterpret_cast<u32x4*>(y)[it] = pack8(o);
+  }
+}
+
+__global__ void __launch_bounds__(256) gelu_bwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+                                                       bf16_t* __restrict__ dx, int64_t n8) {
+  for (int it = blockIdx.x * blockDim.x + threadIdx.x; it < (int)n8; it += gridDim.x * blockDim.x) {
+    float a[8], d[8], o[8];
+    unpack8(reinterpret_cast<const u32x4*>(x)[it], a);
+    unpack8(reinterpret_cast<const u32x4*>(dy)[it], d);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float x2 = a[i] * a[i];
+      const float u = 0.7978845608f * (a[i] + 0.044715f * x2 * a[i]);
+      const float th = tanh_fast(u);
+      const float du = 0.7978845608f * (1.f + 3.f * 0.044715f * x2);
+      o[i] = d[i] * (0.5f * (1.f + th) + 0.5f * a[i] * (1.f - th * th) * du);
+    }
+    reinterpret_cast<u32x4*>(dx)[it] = pack8(o);
+  }
+}
+
+int gelu_fwd(const bf16_t* x, bf16_t* y, int64_t n, hipStream_t stream) {
+  if (n % 8 || n / 8 >= (1ll << 31)) return -1;
+  gelu_fwd_kernel<<<stream_grid(n / 8, 256), 256, 0, stream>>>(x, y, n / 8);
+  return 0;
+}
+int gelu_bwd(const bf16_t* x, const bf16_t* dy, bf16_t* dx, int64_t n, hipStream_t stream) {
+  if (n % 8 || n / 8 >= (1ll << 31)) return -1;
+  gelu_bwd_kernel<<<stream_grid(n / 8, 256), 256, 0, stream>>>(x, dy, dx, n / 8);
+  return 0;
+}
+
+}  // namespace kop

@@ -1,0 +1,48 @@
+// Host-side launcher declarations for every HIP kernel of kubeoperator_amd (gfx950).
+// Each returns 0 on success or a negative code for an unsupported shape; all are asynchronous on
+// `stream` and capture-safe (no allocation, no synchronisation).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+namespace kop {
+typedef uint16_t bf16_t;
+
+// norms.hip
+int norm_fwd(const bf16_t* x, const bf16_t* r, const bf16_t* w, const bf16_t* b, bf16_t* y, bf16_t* s_out, float* rstd,
+             float* mean, int rows, int H, float eps, bool layernorm, hipStream_t stream);
+int norm_bwd_partial_rows(int rows);
+int norm_bwd(const bf16_t* dy, const bf16_t* s, const bf16_t* w, const float* rstd, const float* mean,
+             const bf16_t* dres, bf16_t* dx, float* part, bf16_t* dw, bf16_t* db, int rows, int H, bool layernorm,
+             int accumulate, hipStream_t stream);
+
+// elementwise.hip
+int rope_inplace(bf16_t* x, const float* cos_t, const float* sin_t, const int* pos, int64_t T, int S, int nheads,
+                 int D, int64_t row_stride, bool inverse, hipStream_t stream);
+int swiglu_fwd(const bf16_t* gu, bf16_t* h, int64_t T, int F, hipStream_t stream);
+int swiglu_bwd(const bf16_t* gu, const bf16_t* dh, bf16_t* dgu, int64_t T, int F, hipStream_t stream);
+int gelu_fwd(const bf16_t* x, bf16_t* y, int64_t n, hipStream_t stream);
+int gelu_bwd(const bf16_t* x, const bf16_t* dy, bf16_t* dx, int64_t n, hipStream_t stream);
+
+// cross_entropy.hip
+int cross_entropy_fwd(bf16_t* logits, int64_t ld, int64_t T, int V, const int64_t* tgt, int64_t ignore_index,
+                      float* scale, float* loss_rows, float* lse_rows, bool write_grad, float grad_multiplier,
+                      hipStream_t stream);
+
+// adamw.hip
+int adamw_step(bf16_t* p, const bf16_t* g, float* master, float* m, float* v, int64_t n, float lr, float b1, float b2,
+               float eps, float wd, int step, float gscale, const float* gscale_dev, hipStream_t stream);
+int grad_sumsq(const bf16_t* g, int64_t n, float* out, hipStream_t stream);
+int clip_coef(const float* sumsq, float max_norm, float* coef, float* norm_out, hipStream_t stream);
+
+// flash_attn.hip
+int flash_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int S, int Hq,
+                   int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, float scale, bool causal,
+                   hipStream_t stream);
+size_t flash_attn_bwd_workspace(int B, int S, int Hq, int D);
+int flash_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
+                   const float* lse, bf16_t* dq, bf16_t* dk, bf16_t* dv, void* workspace, int B, int S, int Hq,
+                   int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, int64_t dos, int64_t dqs,
+                   int64_t dks, int64_t dvs, float scale, bool causal, hipStream_t stream);
+}  // namespace kop

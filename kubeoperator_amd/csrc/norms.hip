@@ -1,0 +1,282 @@
+// RMSNorm / LayerNorm forward + backward for gfx950, with the residual add fused in.
+//
+//   forward :  s = x (+ r)            (the residual stream, written out when r is given)
+//              y = norm(s) * w (+ b)  (bf16), rstd (and mean for LayerNorm) saved per row in fp32
+//   backward:  ds = dnorm(dy) (+ ds_resid)   -- the residual-stream gradient flows straight through
+//              dw (+ db) = sum over rows, two-stage: per-block fp32 partial rows, then a column reduce
+//              that writes (or accumulates into) the bf16 gradient buffer slice of the parameter.
+//
+// Memory-bound: every row is read once as 16-byte vectors (8 bf16 per lane per load, Guideline 13)
+// and kept in registers between the statistics pass and the output pass. One 64..256-thread block
+// per row, grid-strided.
+#include "common.h"
+#include "kernels.h"
+
+namespace kop {
+
+template <int NV, bool LN, bool HAS_RES>
+__global__ void __launch_bounds__(256) norm_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ r,
+                                                       const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
+                                                       bf16_t* __restrict__ y, bf16_t* __restrict__ s_out,
+                                                       float* __restrict__ rstd_out, float* __restrict__ mean_out,
+                                                       int rows, int H, float eps) {
+  __shared__ float red[4];
+  const int C = H >> 3;  // 16-byte chunks per row
+  const int nw = blockDim.x >> 6;
+  float wv[NV][8], bv[NV][8];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int c = threadIdx.x + v * blockDim.x;
+    if (c < C) {
+      unpack8(reinterpret_cast<const u32x4*>(w)[c], wv[v]);
+      if (LN) unpack8(reinterpret_cast<const u32x4*>(b)[c], bv[v]);
+    }
+  }
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const u32x4* xr = reinterpret_cast<const u32x4*>(x + (size_t)row * H);
+    float f[NV][8];
+    float acc = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = threadIdx.x + v * blockDim.x;
+      if (c < C) {
+        unpack8(xr[c], f[v]);
+        if (HAS_RES) {
+          float g[8];
+          unpack8(reinterpret_cast<const u32x4*>(r + (size_t)row * H)[c], g);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) f[v][i] += g[i];
+          // the residual stream is carried in bf16: normalise exactly what is stored
+          u32x4 pk = pack8(f[v]);
+          reinterpret_cast<u32x4*>(s_out + (size_t)row * H)[c] = pk;
+          unpack8(pk, f[v]);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc += LN ? f[v][i] : f[v][i] * f[v][i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) f[v][i] = 0.f;
+      }
+    }
+    float mean = 0.f;
+    if (LN) {
+      float t = wave_sum(acc);
+      __syncthreads();
+      if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+      __syncthreads();
+      t = 0.f;
+      for (int i = 0; i < nw; ++i) t += red[i];
+      mean = t / H;
+      acc = 0.f;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        const int c = threadIdx.x + v * blockDim.x;
+        if (c < C) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const float d = f[v][i] - mean;
+            acc += d * d;
+          }
+        }
+      }
+    }
+    float t = wave_sum(acc);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+    __syncthreads();
+    t = 0.f;
+    for (int i = 0; i < nw; ++i) t += red[i];
+    const float rstd = rsqrtf(t / H + eps);
+    if (threadIdx.x == 0) {
+      rstd_out[row] = rstd;
+      if (LN) mean_out[row] = mean;
+    }
+    u32x4* yr = reinterpret_cast<u32x4*>(y + (size_t)row * H);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = threadIdx.x + v * blockDim.x;
+      if (c < C) {
+        float o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = (f[v][i] - mean) * rstd * wv[v][i] + (LN ? bv[v][i] : 0.f);
+        yr[c] = pack8(o);
+      }
+    }
+  }
+}
+
+template <int NV, bool LN, bool HAS_DRES>
+__global__ void __launch_bounds__(256) norm_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s,
+                                                       const bf16_t* __restrict__ w, const float* __restrict__ rstd_in,
+                                                       const float* __restrict__ mean_in,
+                                                       const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx,
+                                                       float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                       int rows, int H) {
+  __shared__ float red[8];
+  const int C = H >> 3;
+  const int nw = blockDim.x >> 6;
+  float wv[NV][8], dwa[NV][8], dba[NV][8];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int c = threadIdx.x + v * blockDim.x;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dwa[v][i] = dba[v][i] = 0.f;
+    if (c < C) unpack8(reinterpret_cast<const u32x4*>(w)[c], wv[v]);
+  }
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const float rstd = rstd_in[row];
+    const float mean = LN ? mean_in[row] : 0.f;
+    float xh[NV][8], g[NV][8];
+    float a1 = 0.f, a2 = 0.f;  // sum(g*xhat), sum(g)
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = threadIdx.x + v * blockDim.x;
+      if (c < C) {
+        float d[8];
+        unpack8(reinterpret_cast<const u32x4*>(s + (size_t)row * H)[c], xh[v]);
+        unpack8(reinterpret_cast<const u32x4*>(dy + (size_t)row * H)[c], d);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          xh[v][i] = (xh[v][i] - mean) * rstd;
+          g[v][i] = d[i] * wv[v][i];
+          dwa[v][i] += d[i] * xh[v][i];
+          if (LN) dba[v][i] += d[i];
+          a1 += g[v][i] * xh[v][i];
+          a2 += g[v][i];
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) xh[v][i] = g[v][i] = 0.f;
+      }
+    }
+    a1 = wave_sum(a1);
+    if (LN) a2 = wave_sum(a2);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+      red[threadIdx.x >> 6] = a1;
+      red[4 + (threadIdx.x >> 6)] = a2;
+    }
+    __syncthreads();
+    a1 = 0.f;
+    a2 = 0.f;
+    for (int i = 0; i < nw; ++i) {
+      a1 += red[i];
+      a2 += red[4 + i];
+    }
+    const float m1 = a1 / H, m2 = a2 / H;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = threadIdx.x + v * blockDim.x;
+      if (c < C) {
+        float o[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = rstd * (g[v][i] - xh[v][i] * m1 - (LN ? m2 : 0.f));
+        if (HAS_DRES) {
+          float d2[8];
+          unpack8(reinterpret_cast<const u32x4*>(dres + (size_t)row * H)[c], d2);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] += d2[i];
+        }
+        reinterpret_cast<u32x4*>(dx + (size_t)row * H)[c] = pack8(o);
+      }
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int c = threadIdx.x + v * blockDim.x;
+    if (c < C) {
+      f32x4* p = reinterpret_cast<f32x4*>(dw_part + (size_t)blockIdx.x * H + c * 8);
+      p[0] = f32x4{dwa[v][0], dwa[v][1], dwa[v][2], dwa[v][3]};
+      p[1] = f32x4{dwa[v][4], dwa[v][5], dwa[v][6], dwa[v][7]};
+      if (LN) {
+        f32x4* q = reinterpret_cast<f32x4*>(db_part + (size_t)blockIdx.x * H + c * 8);
+        q[0] = f32x4{dba[v][0], dba[v][1], dba[v][2], dba[v][3]};
+        q[1] = f32x4{dba[v][4], dba[v][5], dba[v][6], dba[v][7]};
+      }
+    }
+  }
+}
+
+// Column reduce of [nparts, H] fp32 partials into a bf16 gradient (overwrite or accumulate).
+__global__ void __launch_bounds__(256) col_reduce_kernel(const float* __restrict__ part, int nparts, int H,
+                                                         bf16_t* __restrict__ out, int accumulate) {
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int seg = threadIdx.x >> 6;  // 4 row segments per block
+  __shared__ float red[4][64];
+  float a = 0.f;
+  if (col < H)
+    for (int p = seg; p < nparts; p += 4) a += part[(size_t)p * H + col];
+  red[seg][threadIdx.x & 63] = a;
+  __syncthreads();
+  if (seg == 0 && col < H) {
+    float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    if (accumulate) t += bf2f(out[col]);
+    out[col] = f2bf(t);
+  }
+}
+
+static void pick_geom(int H, int& threads, int& nv) {
+  const int C = H / 8;
+  threads = C >= 256 ? 256 : ((C + 63) / 64) * 64;
+  nv = (C + threads - 1) / threads;
+}
+
+#define NORM_FWD_DISPATCH(NVv)                                                                              \
+  if (nv == NVv) {                                                                                          \
+    if (layernorm) {                                                                                        \
+      if (r) norm_fwd_kernel<NVv, true, true><<<grid, threads, 0, stream>>>(x, r, w, b, y, s_out, rstd, mean, rows, H, eps); \
+      else norm_fwd_kernel<NVv, true, false><<<grid, threads, 0, stream>>>(x, r, w, b, y, s_out, rstd, mean, rows, H, eps); \
+    } else {                                                                                                \
+      if (r) norm_fwd_kernel<NVv, false, true><<<grid, threads, 0, stream>>>(x, r, w, b, y, s_out, rstd, mean, rows, H, eps); \
+      else norm_fwd_kernel<NVv, false, false><<<grid, threads, 0, stream>>>(x, r, w, b, y, s_out, rstd, mean, rows, H, eps); \
+    }                                                                                                       \
+    return 0;                                                                                               \
+  }
+
+int norm_fwd(const bf16_t* x, const bf16_t* r, const bf16_t* w, const bf16_t* b, bf16_t* y, bf16_t* s_out, float* rstd,
+             float* mean, int rows, int H, float eps, bool layernorm, hipStream_t stream) {
+  if (H % 8 != 0 || H > 8192) return -1;
+  int threads, nv;
+  pick_geom(H, threads, nv);
+  const int grid = rows < 8192 ? rows : 8192;
+  NORM_FWD_DISPATCH(1)
+  NORM_FWD_DISPATCH(2)
+  NORM_FWD_DISPATCH(3)
+  NORM_FWD_DISPATCH(4)
+  return -2;
+}
+
+#define NORM_BWD_DISPATCH(NVv)                                                                               \
+  if (nv == NVv) {                                                                                           \
+    if (layernorm) {                                                                                         \
+      if (dres) norm_bwd_kernel<NVv, true, true><<<grid, threads, 0, stream>>>(dy, s, w, rstd, mean, dres, dx, part, part + (size_t)grid * H, rows, H); \
+      else norm_bwd_kernel<NVv, true, false><<<grid, threads, 0, stream>>>(dy, s, w, rstd, mean, dres, dx, part, part + (size_t)grid * H, rows, H); \
+    } else {                                                                                                 \
+      if (dres) norm_bwd_kernel<NVv, false, true><<<grid, threads, 0, stream>>>(dy, s, w, rstd, mean, dres, dx, part, nullptr, rows, H); \
+      else norm_bwd_kernel<NVv, false, false><<<grid, threads, 0, stream>>>(dy, s, w, rstd, mean, dres, dx, part, nullptr, rows, H); \
+    }                                                                                                        \
+    done = true;                                                                                             \
+  }
+
+int norm_bwd_partial_rows(int rows) { return rows < 512 ? rows : 512; }
+
+int norm_bwd(const bf16_t* dy, const bf16_t* s, const bf16_t* w, const float* rstd, const float* mean,
+             const bf16_t* dres, bf16_t* dx, float* part, bf16_t* dw, bf16_t* db, int rows, int H, bool layernorm,
+             int accumulate, hipStream_t stream) {
+  if (H % 8 != 0 || H > 8192) return -1;
+  int threads, nv;
+  pick_geom(H, threads, nv);
+  const int grid = norm_bwd_partial_rows(rows);
+  bool done = false;
+  NORM_BWD_DISPATCH(1)
+  NORM_BWD_DISPATCH(2)
+  NORM_BWD_DISPATCH(3)
+  NORM_BWD_DISPATCH(4)
+  if (!done) return -2;
+  const int cg = (H + 63) / 64;
+  col_reduce_kernel<<<cg, 256, 0, stream>>>(part, grid, H, dw, accumulate);
+  if (layernorm) col_reduce_kernel<<<cg, 256, 0, stream>>>(part + (size_t)grid * H, grid, H, db, accumulate);
+  return 0;
+}
+
+}  // namespace kop

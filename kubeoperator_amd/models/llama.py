@@ -1,0 +1,107 @@
+"""Llama-3 decoder (the bundled chart's headline model), built on the gfx950 kernels.
+
+Token activations are kept 2-D ``[B*S, hidden]`` end to end so every projection is one hipBLASLt GEMM and
+every elementwise/normalisation kernel streams contiguous rows. Per block:
+
+    y1, x1 = rmsnorm(x + pending)        fused residual-add + RMSNorm (one kernel)
+    qkv    = y1 @ Wqkv^T                 fused Q|K|V projection, [T, (Hq + 2 Hkv) * 128]
+    a      = flash_attn(rope(qkv))       RoPE in place on the Q/K columns, attention reads the strided
+                                         Q/K/V column views directly (no split / transpose copies)
+    y2, x2 = rmsnorm(x1 + a @ Wo^T)
+    m      = swiglu(y2 @ Wgu^T) @ Wd^T   fused gate|up projection, SwiGLU kernel
+    -> (x2, m)                           the residual add of m is fused into the next block's norm
+
+The LM head and the cross-entropy are one autograd node whose logits buffer is overwritten by its own
+gradient (``ops.cross_entropy_lmhead``). Weight gradients are written straight into the flat gradient
+buffer (see ``parallel.flat``).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from ..ops import functional as kf
+from ..ops.reference import rope_cache
+from ..parallel.flat import ParamSpec
+from .config import ModelConfig
+
+
+class LlamaBlock(nn.Module):
+    def __init__(self, cfg: ModelConfig):
+        super().__init__()
+        H, D = cfg.hidden, cfg.head_dim
+        self.cfg = cfg
+        self.attn_norm = nn.Parameter(torch.empty(H))
+        self.wqkv = nn.Parameter(torch.empty((cfg.n_heads + 2 * cfg.n_kv_heads) * D, H))
+        self.wo = nn.Parameter(torch.empty(H, cfg.n_heads * D))
+        self.mlp_norm = nn.Parameter(torch.empty(H))
+        self.w_gate_up = nn.Parameter(torch.empty(2 * cfg.ffn_hidden, H))
+        self.w_down = nn.Parameter(torch.empty(H, cfg.ffn_hidden))
+
+    def forward(self, x, pending, cos, sin, B, S):
+        c = self.cfg
+        if pending is None:
+            y, x1 = kf.rms_norm(x, self.attn_norm, c.norm_eps), x
+        else:
+            y, x1 = kf.rms_norm(x, self.attn_norm, c.norm_eps, residual=pending)
+        qkv = kf.linear(y, self.wqkv)
+        a = kf.rope_attention(qkv, cos, sin, B, S, c.n_heads, c.n_kv_heads, c.head_dim, causal=True)
+        a = kf.linear(a, self.wo)
+        y2, x2 = kf.rms_norm(x1, self.mlp_norm, c.norm_eps, residual=a)
+        h = kf.swiglu(kf.linear(y2, self.w_gate_up))
+        return x2, kf.linear(h, self.w_down)
+
+
+class Llama(nn.Module):
+    def __init__(self, cfg: ModelConfig):
+        super().__init__()
+        assert cfg.arch == "llama"
+        self.cfg = cfg
+        self.tok_emb = nn.Parameter(torch.empty(cfg.vocab_size, cfg.hidden))
+        self.layers = nn.ModuleList([LlamaBlock(cfg) for _ in range(cfg.n_layers)])
+        self.final_norm = nn.Parameter(torch.empty(cfg.hidden))
+        if not cfg.tie_embeddings:
+            self.lm_head = nn.Parameter(torch.empty(cfg.vocab_size, cfg.hidden))
+        self._rope = {}
+
+    # flat layout: reverse order of gradient readiness in backward; norms in the no-decay region
+    def param_specs(self) -> list[ParamSpec]:
+        c = self.cfg
+        std = c.init_std
+        out_std = std / math.sqrt(2 * c.n_layers)
+        specs = []
+        if not c.tie_embeddings:
+            specs.append(ParamSpec("lm_head", self.lm_head, True, 1, "normal", std))
+        for i in reversed(range(c.n_layers)):
+            L = self.layers[i]
+            specs += [
+                ParamSpec(f"layers.{i}.w_down", L.w_down, True, 1, "normal", out_std),
+                ParamSpec(f"layers.{i}.w_gate_up", L.w_gate_up, True, 1, "normal", std),
+                ParamSpec(f"layers.{i}.wo", L.wo, True, 1, "normal", out_std),
+                ParamSpec(f"layers.{i}.wqkv", L.wqkv, True, 1, "normal", std),
+            ]
+        specs.append(ParamSpec("tok_emb", self.tok_emb, True, 2 if c.tie_embeddings else 1, "normal", std))
+        specs.append(ParamSpec("final_norm", self.final_norm, False, 1, "ones"))
+        for i in reversed(range(c.n_layers)):
+            specs.append(ParamSpec(f"layers.{i}.mlp_norm", self.layers[i].mlp_norm, False, 1, "ones"))
+            specs.append(ParamSpec(f"layers.{i}.attn_norm", self.layers[i].attn_norm, False, 1, "ones"))
+        return specs
+
+    def rope_tables(self, S, device):
+        key = (S, str(device))
+        if key not in self._rope:
+            self._rope[key] = rope_cache(S, self.cfg.head_dim, self.cfg.rope_theta, device=device)
+        return self._rope[key]
+
+    def forward(self, ids: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
+        B, S = ids.shape
+        cos, sin = self.rope_tables(S, ids.device)
+        x = kf.embedding(ids.reshape(-1), self.tok_emb)
+        pending = None
+        for blk in self.layers:
+            x, pending = blk(x, pending, cos, sin, B, S)
+        y, _ = kf.rms_norm(x, self.final_norm, self.cfg.norm_eps, residual=pending)
+        head = self.tok_emb if self.cfg.tie_embeddings else self.lm_head
+        return kf.cross_entropy_lmhead(y, head, targets.reshape(-1))

@@ -1,0 +1,339 @@
+"""Autograd wrappers around the gfx950 kernels.
+
+GPU tensors always take the HIP path (``ops.load()`` raises if the extension is missing); CPU tensors take
+the fp32 reference path so the whole trainer can be exercised in CPU-only CI.
+
+Weight gradients follow the flat-buffer protocol of :class:`kubeoperator_amd.parallel.flat.FlatParamStore`:
+a parameter that carries ``main_grad`` (a view into the store's flat bf16 gradient buffer) gets its gradient
+written (or accumulated, for gradient-accumulation micro-batches) straight into that view by the backward
+kernel / GEMM (``torch.mm(..., out=main_grad)``), and the store is notified so the data-parallel layer can
+launch the bucket's collective immediately -- no AccumulateGrad pass, no extra copy.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+from torch.autograd import Function
+
+from . import reference as ref
+
+
+def _lib():
+    from . import load
+
+    return load()
+
+
+# ---------------------------------------------------------------------------------------------------
+# weight-gradient sink
+# ---------------------------------------------------------------------------------------------------
+def _sink(w: torch.Tensor, produce):
+    """``produce(out, accumulate)`` writes the gradient of ``w``; returns what autograd should receive."""
+    mg = getattr(w, "main_grad", None)
+    if mg is None:
+        g = torch.empty_like(w)
+        produce(g, False)
+        return g
+    hooks = w._kop_hooks
+    produce(mg, hooks.accumulate_for(w))
+    hooks.ready(w)
+    return None
+
+
+def _mm_into(a, b, out, accumulate):
+    if accumulate:
+        out.addmm_(a, b)
+    else:
+        torch.mm(a, b, out=out)
+
+
+# ---------------------------------------------------------------------------------------------------
+# linear
+# ---------------------------------------------------------------------------------------------------
+class _Linear(Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        x2 = x.reshape(-1, x.shape[-1])
+        y = torch.addmm(b, x2, w.t()) if b is not None else torch.mm(x2, w.t())
+        ctx.save_for_backward(x2, w)
+        ctx.has_b = b is not None
+        if b is not None:
+            ctx.b = b
+        ctx.in_shape = x.shape
+        return y.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, w.shape[0])
+        dx = torch.mm(dy2, w).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
+        dw = _sink(w, lambda out, acc: _mm_into(dy2.t(), x2, out, acc)) if ctx.needs_input_grad[1] else None
+        db = None
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            def prod(out, acc):
+                s = dy2.sum(0, dtype=torch.float32)
+                if acc:
+                    out.add_(s.to(out.dtype))
+                else:
+                    out.copy_(s)
+            db = _sink(ctx.b, prod)
+        return dx, dw, db
+
+
+def linear(x, w, b=None):
+    if not x.is_cuda:
+        return F.linear(x, w, b)
+    return _Linear.apply(x, w, b)
+
+
+# ---------------------------------------------------------------------------------------------------
+# RMSNorm / LayerNorm with fused residual add
+# ---------------------------------------------------------------------------------------------------
+class _Norm(Function):
+    @staticmethod
+    def forward(ctx, x, residual, w, b, eps, layernorm):
+        lib = _lib()
+        x = x.contiguous()
+        y, s, rstd, mean = lib.norm_fwd(x, residual.contiguous() if residual is not None else None, w, b, eps, layernorm)
+        has_res = residual is not None
+        if not has_res:
+            s = x
+        ctx.save_for_backward(s, w, rstd, mean if layernorm else None)
+        ctx.layernorm = layernorm
+        ctx.has_res = has_res
+        ctx.b = b
+        if has_res:
+            return y, s
+        return y
+
+    @staticmethod
+    def backward(ctx, dy, ds_extra=None):
+        lib = _lib()
+        s, w, rstd, mean = ctx.saved_tensors
+        dy = dy.contiguous()
+        dres = ds_extra.contiguous() if ds_extra is not None else None
+        dw_holder = {}
+        db_holder = {}
+
+        b = ctx.b
+        need_w = ctx.needs_input_grad[2]
+        mg_w = getattr(w, "main_grad", None) if need_w else None
+        mg_b = getattr(b, "main_grad", None) if (b is not None and ctx.needs_input_grad[3]) else None
+        dw_buf = mg_w if mg_w is not None else torch.empty_like(w)
+        db_buf = None
+        if ctx.layernorm:
+            db_buf = mg_b if mg_b is not None else torch.empty_like(b)
+        acc = w._kop_hooks.accumulate_for(w) if mg_w is not None else False
+        dx = lib.norm_bwd(dy, s, w, rstd, mean, dres, dw_buf, db_buf, ctx.layernorm, acc)
+        dw = None
+        if need_w:
+            if mg_w is not None:
+                w._kop_hooks.ready(w)
+            else:
+                dw = dw_buf
+        db = None
+        if ctx.layernorm and ctx.needs_input_grad[3]:
+            if mg_b is not None:
+                b._kop_hooks.ready(b)
+            else:
+                db = db_buf
+        del dw_holder, db_holder
+        dres_out = dx if ctx.has_res else None
+        return dx, dres_out, dw, db, None, None
+
+
+def rms_norm(x, w, eps=1e-5, residual=None):
+    """y = rmsnorm(x (+ residual)) * w; returns y, or (y, x + residual) when residual is given."""
+    if not x.is_cuda:
+        y, s = ref.rms_norm_ref(x, w, eps, residual)
+        return (y, s) if residual is not None else y
+    return _Norm.apply(x, residual, w, None, eps, False)
+
+
+def layer_norm(x, w, b, eps=1e-5, residual=None):
+    if not x.is_cuda:
+        y, s = ref.layer_norm_ref(x, w, b, eps, residual)
+        return (y, s) if residual is not None else y
+    return _Norm.apply(x, residual, w, b, eps, True)
+
+
+# ---------------------------------------------------------------------------------------------------
+# SwiGLU / GELU
+# ---------------------------------------------------------------------------------------------------
+class _SwiGLU(Function):
+    @staticmethod
+    def forward(ctx, gu):
+        gu = gu.contiguous()
+        ctx.save_for_backward(gu)
+        return _lib().swiglu_fwd(gu)
+
+    @staticmethod
+    def backward(ctx, dh):
+        (gu,) = ctx.saved_tensors
+        return _lib().swiglu_bwd(gu, dh.contiguous())
+
+
+def swiglu(gu):
+    if not gu.is_cuda:
+        g, u = gu.chunk(2, dim=-1)
+        return F.silu(g) * u
+    return _SwiGLU.apply(gu)
+
+
+class _GELU(Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        ctx.save_for_backward(x)
+        return _lib().gelu_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        return _lib().gelu_bwd(x, dy.contiguous())
+
+
+def gelu(x):
+    if not x.is_cuda:
+        return F.gelu(x, approximate="tanh")
+    return _GELU.apply(x)
+
+
+# ---------------------------------------------------------------------------------------------------
+# attention (RoPE + flash attention on the fused QKV activation)
+# ---------------------------------------------------------------------------------------------------
+class _RopeAttention(Function):
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, B, S, Hq, Hkv, D, causal, scale, use_rope):
+        lib = _lib()
+        qkv = qkv.contiguous()
+        if use_rope:
+            lib.rope_(qkv, cos, sin, None, S, Hq + Hkv, D, False)
+        q = qkv[:, : Hq * D]
+        k = qkv[:, Hq * D:(Hq + Hkv) * D]
+        v = qkv[:, (Hq + Hkv) * D:]
+        T = qkv.shape[0]
+        o = torch.empty(T, Hq * D, dtype=qkv.dtype, device=qkv.device)
+        lse = torch.empty(B * Hq * S, dtype=torch.float32, device=qkv.device)
+        lib.flash_attn_fwd(q, k, v, o, lse, B, S, Hq, Hkv, D, scale, causal)
+        ctx.save_for_backward(qkv, o, lse, cos, sin)
+        ctx.cfg = (B, S, Hq, Hkv, D, causal, scale, use_rope)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        lib = _lib()
+        qkv, o, lse, cos, sin = ctx.saved_tensors
+        B, S, Hq, Hkv, D, causal, scale, use_rope = ctx.cfg
+        do = do.contiguous()
+        dqkv = torch.empty_like(qkv)
+        ws = torch.empty(lib.flash_attn_bwd_workspace(B, S, Hq, D), dtype=torch.uint8, device=qkv.device)
+        a, c = Hq * D, (Hq + Hkv) * D
+        lib.flash_attn_bwd(qkv[:, :a], qkv[:, a:c], qkv[:, c:], o, do, lse, dqkv[:, :a], dqkv[:, a:c], dqkv[:, c:], ws,
+                           B, S, Hq, Hkv, D, scale, causal)
+        if use_rope:
+            lib.rope_(dqkv, cos, sin, None, S, Hq + Hkv, D, True)
+        return dqkv, None, None, None, None, None, None, None, None, None, None
+
+
+def rope_attention(qkv, cos, sin, B, S, Hq, Hkv, D, causal=True, scale=None, use_rope=True):
+    """Fused-QKV activation [B*S, (Hq+2Hkv)*D] -> attention output [B*S, Hq*D] (RoPE on Q,K if use_rope)."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if not qkv.is_cuda:
+        x = ref.rope_ref(qkv, cos, sin, S, Hq + Hkv, D) if use_rope else qkv
+        a, c = Hq * D, (Hq + Hkv) * D
+        o, _ = _attn_ref_autograd(x[:, :a], x[:, a:c], x[:, c:], B, S, Hq, Hkv, D, causal, scale)
+        return o
+    return _RopeAttention.apply(qkv, cos, sin, B, S, Hq, Hkv, D, causal, scale, use_rope)
+
+
+def _attn_ref_autograd(q, k, v, B, S, Hq, Hkv, D, causal, scale):
+    qh = q.reshape(B, S, Hq, D).transpose(1, 2)
+    kh = k.reshape(B, S, Hkv, D).transpose(1, 2).repeat_interleave(Hq // Hkv, dim=1)
+    vh = v.reshape(B, S, Hkv, D).transpose(1, 2).repeat_interleave(Hq // Hkv, dim=1)
+    o = F.scaled_dot_product_attention(qh, kh, vh, is_causal=causal, scale=scale)
+    return o.transpose(1, 2).reshape(B * S, Hq * D), None
+
+
+def flash_attention(q, k, v, B, S, Hq, Hkv, D, causal=True, scale=None):
+    """Attention on already-positioned q/k/v row views; returns (o, lse). Forward only helper for tests."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if not q.is_cuda:
+        return ref.attention_ref(q, k, v, B, S, Hq, Hkv, D, causal, scale)
+    lib = _lib()
+    o = torch.empty(B * S, Hq * D, dtype=q.dtype, device=q.device)
+    lse = torch.empty(B * Hq * S, dtype=torch.float32, device=q.device)
+    lib.flash_attn_fwd(q, k, v, o, lse, B, S, Hq, Hkv, D, scale, causal)
+    return o, lse.view(B, Hq, S)
+
+
+# ---------------------------------------------------------------------------------------------------
+# embedding
+# ---------------------------------------------------------------------------------------------------
+class _Embedding(Function):
+    @staticmethod
+    def forward(ctx, ids, w):
+        ctx.save_for_backward(ids)
+        ctx.V = w.shape[0]
+        ctx.w = w
+        return F.embedding(ids, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (ids,) = ctx.saved_tensors
+        w = ctx.w
+        H = w.shape[1]
+
+        def prod(out, acc):
+            g = torch.ops.aten.embedding_dense_backward(dy.reshape(-1, H), ids.reshape(-1), ctx.V, -1, False)
+            if acc:
+                out.add_(g)
+            else:
+                out.copy_(g)
+
+        return None, _sink(w, prod)
+
+
+def embedding(ids, w):
+    if not w.is_cuda:
+        return F.embedding(ids, w)
+    return _Embedding.apply(ids, w)
+
+
+# ---------------------------------------------------------------------------------------------------
+# LM head + cross entropy (fused: logits buffer is overwritten by its own gradient)
+# ---------------------------------------------------------------------------------------------------
+class _LMHeadCE(Function):
+    @staticmethod
+    def forward(ctx, x, w, targets, ignore_index):
+        lib = _lib()
+        x2 = x.reshape(-1, x.shape[-1]).contiguous()
+        logits = torch.mm(x2, w.t())
+        loss_rows, lse, scale = lib.cross_entropy_fwd_(logits, targets.reshape(-1).contiguous(), ignore_index, True, 1.0)
+        loss = loss_rows.sum() * scale[0]
+        ctx.save_for_backward(x2, w, logits)
+        ctx.in_shape = x.shape
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        x2, w, dlogits = ctx.saved_tensors
+        g = g.to(torch.float32)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = (torch.mm(dlogits, w) * g).view(ctx.in_shape)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            xg = x2 * g
+            dw = _sink(w, lambda out, acc: _mm_into(dlogits.t(), xg, out, acc))
+        return dx, dw, None, None
+
+
+def cross_entropy_lmhead(x, w, targets, ignore_index=-100):
+    """mean cross-entropy of softmax(x @ w^T) against targets, computed without fp32 logits."""
+    if not x.is_cuda:
+        logits = F.linear(x.reshape(-1, x.shape[-1]), w)
+        return F.cross_entropy(logits.float(), targets.reshape(-1), ignore_index=ignore_index)
+    return _LMHeadCE.apply(x, w, targets, ignore_index)

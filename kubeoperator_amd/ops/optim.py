@@ -1,0 +1,132 @@
+"""Fused AdamW over flat (segmented) parameter storage.
+
+The optimizer does not see ``nn.Parameter`` objects: it is handed *segments* -- pairs of equally sized
+views into the flat bf16 parameter buffer and the flat bf16 gradient buffer, each with its weight decay --
+and keeps fp32 master weights, exp_avg and exp_avg_sq for all segments in three contiguous fp32 buffers.
+One ``adamw_`` kernel launch per segment (a handful per step: one per weight-decay region, or one per
+ZeRO-1 bucket shard). Gradient clipping is computed on device (sum of squares -> clip coefficient) and fed
+to the kernel as a device scalar, so a step never synchronises with the host.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+
+@dataclass
+class Segment:
+    param: torch.Tensor  # bf16 view (flat)
+    grad: torch.Tensor   # bf16 view (flat), same numel
+    weight_decay: float
+
+
+class FusedAdamW:
+    def __init__(self, segments: list[Segment], lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
+                 weight_decay: float = 0.1, max_grad_norm: float = 1.0, grad_scale: float = 1.0,
+                 norm_allreduce=None):
+        # a segment's weight_decay of None means "the optimizer's default"
+        for sg in segments:
+            if sg.weight_decay is None:
+                sg.weight_decay = weight_decay
+        self.segments = segments
+        self.lr = lr
+        self.b1, self.b2 = betas
+        self.eps = eps
+        self.default_wd = weight_decay
+        self.max_grad_norm = max_grad_norm
+        self.grad_scale = grad_scale
+        self.norm_allreduce = norm_allreduce  # callable(tensor) summing a device scalar across shards
+        self.step_count = 0
+        n = sum(s.param.numel() for s in segments)
+        dev = segments[0].param.device if segments else torch.device("cpu")
+        self.master = torch.empty(n, dtype=torch.float32, device=dev)
+        self.exp_avg = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=dev)
+        self._views = []
+        off = 0
+        for s in segments:
+            k = s.param.numel()
+            self.master[off:off + k].copy_(s.param.reshape(-1).float())
+            self._views.append((off, off + k))
+            off += k
+        self._sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
+        self._coef = torch.ones(1, dtype=torch.float32, device=dev)
+        self.last_grad_norm = torch.zeros(1, dtype=torch.float32, device=dev)
+
+    # -------------------------------------------------------------------------------------------
+    def state_bytes(self) -> int:
+        return self.master.numel() * 4 * 3
+
+    def _native(self) -> bool:
+        return self.master.is_cuda
+
+    def clip(self):
+        """Compute the global grad norm and the clip coefficient on device (no host sync)."""
+        if self.max_grad_norm is None or self.max_grad_norm <= 0:
+            self._coef.fill_(1.0)
+            return
+        self._sumsq.zero_()
+        if self._native():
+            from . import load
+
+            lib = load()
+            for s in self.segments:
+                if s.grad.numel():
+                    lib.grad_sumsq_(s.grad.reshape(-1), self._sumsq)
+        else:
+            for s in self.segments:
+                self._sumsq += s.grad.float().pow(2).sum()
+        if self.grad_scale != 1.0:
+            self._sumsq.mul_(self.grad_scale * self.grad_scale)
+        if self.norm_allreduce is not None:
+            self.norm_allreduce(self._sumsq)
+        if self._native():
+            from . import load
+
+            load().clip_coef_(self._sumsq, float(self.max_grad_norm), self._coef, self.last_grad_norm)
+        else:
+            nrm = self._sumsq.sqrt()
+            self.last_grad_norm.copy_(nrm)
+            self._coef.copy_(torch.clamp(self.max_grad_norm / (nrm + 1e-6), max=1.0))
+
+    def step(self, lr: float | None = None):
+        lr = self.lr if lr is None else lr
+        self.step_count += 1
+        self.clip()
+        if self._native():
+            from . import load
+
+            lib = load()
+            for s, (a, b) in zip(self.segments, self._views):
+                if b == a:
+                    continue
+                lib.adamw_(s.param.reshape(-1), s.grad.reshape(-1), self.master[a:b], self.exp_avg[a:b],
+                           self.exp_avg_sq[a:b], lr, self.b1, self.b2, self.eps, s.weight_decay, self.step_count,
+                           self.grad_scale, self._coef)
+        else:
+            t = self.step_count
+            bc1 = 1 - self.b1 ** t
+            bc2 = 1 - self.b2 ** t
+            for s, (a, b) in zip(self.segments, self._views):
+                g = s.grad.reshape(-1).float() * self.grad_scale * self._coef
+                m, v, w = self.exp_avg[a:b], self.exp_avg_sq[a:b], self.master[a:b]
+                m.mul_(self.b1).add_(g, alpha=1 - self.b1)
+                v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+                w.mul_(1 - lr * s.weight_decay)
+                w.sub_(lr * (m / bc1) / (v.sqrt() / math.sqrt(bc2) + self.eps))
+                s.param.reshape(-1).copy_(w)
+
+    # checkpointing -------------------------------------------------------------------------------
+    def state_dict(self):
+        return {"step": self.step_count, "master": self.master, "exp_avg": self.exp_avg,
+                "exp_avg_sq": self.exp_avg_sq, "lr": self.lr}
+
+    def load_state_dict(self, sd):
+        self.step_count = int(sd["step"])
+        self.master.copy_(sd["master"])
+        self.exp_avg.copy_(sd["exp_avg"])
+        self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+        for s, (a, b) in zip(self.segments, self._views):
+            s.param.reshape(-1).copy_(self.master[a:b])

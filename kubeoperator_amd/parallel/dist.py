@@ -1,0 +1,80 @@
+"""Process-group bootstrap: one process per GPU, ``torch.distributed`` over RCCL (backend "nccl" on ROCm)
+for GPU ranks, gloo for CPU ranks (tests). Reads RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* from the
+environment (torchrun contract); a single process without those variables runs as world size 1 with no
+process group at all.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    local_rank: int = 0
+    world: int = 1
+    backend: str = "none"
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+
+def init_distributed(device: str = "auto", timeout_s: int = 1800) -> DistInfo:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = (device == "cuda") or (device == "auto" and torch.cuda.is_available())
+    if use_gpu:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
+    backend = "none"
+    if world > 1 and not dist.is_initialized():
+        backend = "nccl" if use_gpu else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        kw = {}
+        if use_gpu:
+            kw["device_id"] = dev
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    elif dist.is_initialized():
+        backend = dist.get_backend()
+    return DistInfo(rank, local, world, backend, dev)
+
+
+def barrier(info: DistInfo) -> None:
+    if info.world > 1:
+        if info.backend == "nccl":
+            dist.barrier(device_ids=[info.local_rank])
+        else:
+            dist.barrier()
+
+
+def all_reduce_max(x: float, info: DistInfo) -> float:
+    if info.world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=info.device if info.backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def all_reduce_sum(x: float, info: DistInfo) -> float:
+    if info.world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=info.device if info.backend == "nccl" else "cpu")
+    dist.all_reduce(t)
+    return float(t.item())
+
+
+def shutdown(info: DistInfo) -> None:
+    if info.world > 1 and dist.is_initialized():
+        dist.destroy_process_group()

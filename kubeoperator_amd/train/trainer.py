@@ -1,0 +1,106 @@
+"""Trainer of the bundled PyTorch-ROCm chart: model on the flat bucketed store, RCCL data parallelism,
+fused AdamW with on-device clipping, warmup + cosine LR, gradient accumulation, checkpoint/resume.
+
+A training step never synchronises with the host: the loss is returned as a device tensor and only read
+when logging.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import asdict, dataclass, field
+
+import torch
+
+from ..models import build_model, get_config
+from ..ops.optim import FusedAdamW
+from ..parallel.ddp import DataParallel
+from ..parallel.dist import DistInfo
+from ..parallel.flat import FlatParamStore
+
+
+@dataclass
+class TrainConfig:
+    model: str = "llama3_8b"
+    micro_batch: int = 1
+    seq_len: int = 8192
+    grad_accum: int = 1
+    lr: float = 3e-4
+    min_lr: float = 3e-5
+    warmup_steps: int = 100
+    total_steps: int = 10000
+    weight_decay: float = 0.1
+    betas: tuple = (0.9, 0.95)
+    eps: float = 1e-8
+    grad_clip: float = 1.0
+    dp_mode: str = "allreduce"  # allreduce | zero1
+    bucket_mb: int = 512
+    seed: int = 1234
+    model_overrides: dict = field(default_factory=dict)
+
+    def to_dict(self):
+        return asdict(self)
+
+
+def lr_at(step: int, tc: TrainConfig) -> float:
+    if step < tc.warmup_steps:
+        return tc.lr * (step + 1) / tc.warmup_steps
+    p = min(1.0, (step - tc.warmup_steps) / max(1, tc.total_steps - tc.warmup_steps))
+    return tc.min_lr + 0.5 * (tc.lr - tc.min_lr) * (1 + math.cos(math.pi * p))
+
+
+class Trainer:
+    def __init__(self, tc: TrainConfig, info: DistInfo):
+        self.tc = tc
+        self.info = info
+        self.cfg = get_config(tc.model, **tc.model_overrides)
+        if tc.seq_len > self.cfg.max_seq_len:
+            raise ValueError(f"seq_len {tc.seq_len} > model max_seq_len {self.cfg.max_seq_len}")
+        dev = info.device
+        t0 = time.time()
+        with torch.device("meta"):
+            self.model = build_model(self.cfg)
+        self.store = FlatParamStore(self.model, self.model.param_specs(), dev, world=info.world,
+                                    bucket_bytes=tc.bucket_mb * 1024 * 1024)
+        self.store.init_weights(seed=tc.seed)
+        self.dp = DataParallel(self.store, info, tc.dp_mode)
+        self.dp.broadcast_params()
+        self.opt = FusedAdamW(self.dp.optimizer_segments(), lr=tc.lr, betas=tc.betas, eps=tc.eps,
+                              weight_decay=tc.weight_decay, max_grad_norm=tc.grad_clip,
+                              grad_scale=self.dp.grad_scale / tc.grad_accum, norm_allreduce=self.dp.norm_allreduce())
+        self.step = 0
+        self.setup_seconds = time.time() - t0
+
+    @property
+    def tokens_per_step(self) -> int:
+        """Tokens processed per optimizer step by THIS rank."""
+        return self.tc.micro_batch * self.tc.seq_len * self.tc.grad_accum
+
+    def train_step(self, batches) -> torch.Tensor:
+        """``batches``: iterable of ``grad_accum`` (ids, targets) pairs, each [micro_batch, seq_len]."""
+        losses = []
+        n = self.tc.grad_accum
+        for i, (ids, tgt) in enumerate(batches):
+            self.store.begin_microbatch(i)
+            self.dp.sync = i == n - 1
+            loss = self.model(ids, tgt)
+            loss.backward()
+            losses.append(loss.detach())
+        self.dp.finish_grads()
+        self.opt.step(lr_at(self.step, self.tc))
+        self.dp.after_step()
+        self.step += 1
+        return torch.stack(losses).mean()
+
+    # checkpoint -----------------------------------------------------------------------------------
+    def state_dict(self):
+        return {"step": self.step, "train_config": self.tc.to_dict(), "model_config": self.cfg.to_dict(),
+                "params": self.store.params, "optimizer": self.opt.state_dict(), "world": self.info.world,
+                "rank": self.info.rank, "dp_mode": self.tc.dp_mode}
+
+    def load_state_dict(self, sd):
+        if sd["world"] != self.info.world and self.tc.dp_mode == "zero1":
+            raise ValueError("ZeRO-1 checkpoints are sharded per rank: resume with the same world size")
+        self.store.params.copy_(sd["params"])
+        self.opt.load_state_dict(sd["optimizer"])
+        self.step = int(sd["step"])

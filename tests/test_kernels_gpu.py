@@ -1,0 +1,260 @@
+"""Numerics of every gfx950 HIP kernel against a plain-PyTorch fp32 reference of the same op (GPU only)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def lib():
+    from kubeoperator_amd.ops import load
+
+    return load()
+
+
+def rel_err(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+def test_extension_is_native():
+    m = lib()
+    assert m.__file__.endswith("_C.so")
+    assert m.ARCH == "gfx950"
+    props = torch.cuda.get_device_properties(0)
+    assert "gfx950" in getattr(props, "gcnArchName", "gfx950")
+
+
+@pytest.mark.parametrize("H", [4096, 768, 1024])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_rmsnorm_fwd_bwd(H, with_res):
+    from kubeoperator_amd.ops.functional import rms_norm
+
+    torch.manual_seed(0)
+    T = 333
+    x = torch.randn(T, H, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn(T, H, device=DEV, dtype=torch.bfloat16, requires_grad=True) if with_res else None
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    out = rms_norm(x, w, 1e-5, residual=r)
+    y, s = out if with_res else (out, None)
+    dy = torch.randn_like(y)
+    ds = torch.randn_like(y) if with_res else None
+    loss = (y.float() * dy.float()).sum() + ((s.float() * ds.float()).sum() if with_res else 0)
+    loss.backward()
+    # reference
+    xf = x.detach().float().requires_grad_(True)
+    rf = r.detach().float().requires_grad_(True) if with_res else None
+    wf = w.detach().float().requires_grad_(True)
+    sf = xf + rf if with_res else xf
+    sf_b = sf.to(torch.bfloat16).float() if with_res else sf
+    yf = sf_b * torch.rsqrt(sf_b.pow(2).mean(-1, keepdim=True) + 1e-5) * wf
+    lf = (yf * dy.float()).sum() + ((sf * ds.float()).sum() if with_res else 0)
+    lf.backward()
+    assert rel_err(y, yf) < 2e-2
+    assert rel_err(x.grad, xf.grad) < 3e-2
+    assert rel_err(w.grad, wf.grad) < 3e-2
+    if with_res:
+        assert rel_err(r.grad, rf.grad) < 3e-2
+
+
+@pytest.mark.parametrize("H", [768, 4096])
+def test_layernorm_fwd_bwd(H):
+    from kubeoperator_amd.ops.functional import layer_norm
+
+    torch.manual_seed(1)
+    T = 257
+    x = (torch.randn(T, H, device=DEV) * 2 + 0.5).to(torch.bfloat16).requires_grad_(True)
+    w = (1 + 0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    b = (0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    y = layer_norm(x, w, b, 1e-5)
+    dy = torch.randn_like(y)
+    (y.float() * dy.float()).sum().backward()
+    xf, wf, bf = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    yf = torch.nn.functional.layer_norm(xf, (H,), wf, bf, 1e-5)
+    (yf * dy.float()).sum().backward()
+    assert rel_err(y, yf) < 2e-2
+    assert rel_err(x.grad, xf.grad) < 3e-2
+    assert rel_err(w.grad, wf.grad) < 3e-2
+    assert rel_err(b.grad, bf.grad) < 3e-2
+
+
+@pytest.mark.parametrize("D", [128, 64])
+def test_rope_matches_reference_and_inverts(D):
+    from kubeoperator_amd.ops.reference import rope_cache, rope_ref
+
+    torch.manual_seed(2)
+    S, B, Hq, Hkv = 64, 2, 4, 2
+    cos, sin = rope_cache(S, D, 500000.0, device=DEV)
+    x = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
+    ref = rope_ref(x, cos, sin, S, Hq + Hkv, D)
+    y = x.clone()
+    lib().rope_(y, cos, sin, None, S, Hq + Hkv, D, False)
+    assert rel_err(y, ref) < 1e-2
+    # V columns untouched
+    assert torch.equal(y[:, (Hq + Hkv) * D:], x[:, (Hq + Hkv) * D:])
+    lib().rope_(y, cos, sin, None, S, Hq + Hkv, D, True)
+    assert rel_err(y, x) < 2e-2
+
+
+def test_swiglu_fwd_bwd():
+    from kubeoperator_amd.ops.functional import swiglu
+
+    torch.manual_seed(3)
+    gu = torch.randn(100, 2 * 1536, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    h = swiglu(gu)
+    dh = torch.randn_like(h)
+    (h.float() * dh.float()).sum().backward()
+    g = gu.detach().float().requires_grad_(True)
+    a, b = g.chunk(2, -1)
+    hf = torch.nn.functional.silu(a) * b
+    (hf * dh.float()).sum().backward()
+    assert rel_err(h, hf) < 2e-2
+    assert rel_err(gu.grad, g.grad) < 2e-2
+
+
+def test_gelu_fwd_bwd():
+    from kubeoperator_amd.ops.functional import gelu
+
+    torch.manual_seed(4)
+    x = (3 * torch.randn(64, 3072, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    y = gelu(x)
+    dy = torch.randn_like(y)
+    (y.float() * dy.float()).sum().backward()
+    xf = x.detach().float().requires_grad_(True)
+    yf = torch.nn.functional.gelu(xf, approximate="tanh")
+    (yf * dy.float()).sum().backward()
+    assert rel_err(y, yf) < 2e-2
+    assert rel_err(x.grad, xf.grad) < 2e-2
+
+
+@pytest.mark.parametrize("V", [128256, 50257, 1000])
+def test_cross_entropy_lmhead(V):
+    from kubeoperator_amd.ops.functional import cross_entropy_lmhead
+
+    torch.manual_seed(5)
+    T, H = 96, 256
+    x = (0.5 * torch.randn(T, H, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    w = (0.05 * torch.randn(V, H, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    tgt = torch.randint(0, V, (T,), device=DEV)
+    tgt[::7] = -100
+    loss = cross_entropy_lmhead(x, w, tgt)
+    (loss * 2.0).backward()
+    xf, wf = (t.detach().float().requires_grad_(True) for t in (x, w))
+    logits = (xf @ wf.t()).to(torch.bfloat16).float()
+    lf = torch.nn.functional.cross_entropy(logits, tgt, ignore_index=-100)
+    (lf * 2.0).backward()
+    assert abs(loss.item() - lf.item()) < 1e-2 * max(1.0, lf.item())
+    assert rel_err(x.grad, xf.grad) < 3e-2
+    assert rel_err(w.grad, wf.grad) < 3e-2
+
+
+def test_adamw_matches_reference():
+    from kubeoperator_amd.ops.optim import FusedAdamW, Segment
+
+    torch.manual_seed(6)
+    n = 4096 * 3 + 64
+    p = torch.randn(n, device=DEV).to(torch.bfloat16)
+    g = (0.01 * torch.randn(n, device=DEV)).to(torch.bfloat16)
+    opt = FusedAdamW([Segment(p[: n // 2], g[: n // 2], 0.1), Segment(p[n // 2:], g[n // 2:], 0.0)], lr=1e-3,
+                     max_grad_norm=0.5)
+    master = p.float().clone()
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    for step in range(1, 4):
+        opt.step()
+        gf = g.float()
+        coef = min(1.0, 0.5 / (gf.norm().item() + 1e-6))
+        gf = gf * coef
+        m.mul_(0.9).add_(gf, alpha=0.1)
+        v.mul_(0.95).addcmul_(gf, gf, value=0.05)
+        wd = torch.cat([torch.full((n // 2,), 0.1, device=DEV), torch.zeros(n - n // 2, device=DEV)])
+        master.mul_(1 - 1e-3 * wd)
+        master.sub_(1e-3 * (m / (1 - 0.9 ** step)) / ((v / (1 - 0.95 ** step)).sqrt() + 1e-8))
+    assert rel_err(opt.master, master) < 1e-5
+    assert rel_err(p, master) < 1e-2
+    assert abs(opt.last_grad_norm.item() - g.float().norm().item()) < 1e-3 * g.float().norm().item()
+
+
+def _attn_case(B, S, Hq, Hkv, D, causal, seed=7):
+    from kubeoperator_amd.ops.functional import flash_attention
+    from kubeoperator_amd.ops.reference import attention_ref
+
+    torch.manual_seed(seed)
+    qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
+    a, c = Hq * D, (Hq + Hkv) * D
+    o, lse = flash_attention(qkv[:, :a], qkv[:, a:c], qkv[:, c:], B, S, Hq, Hkv, D, causal)
+    o_ref, lse_ref = attention_ref(qkv[:, :a], qkv[:, a:c], qkv[:, c:], B, S, Hq, Hkv, D, causal)
+    return o, lse, o_ref, lse_ref
+
+
+@pytest.mark.parametrize("D", [128, 64])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_fwd(D, causal):
+    o, lse, o_ref, lse_ref = _attn_case(2, 256, 8, 2, D, causal)
+    assert rel_err(o, o_ref) < 2e-2
+    assert (lse - lse_ref).abs().max().item() < 2e-2
+
+
+def test_flash_attention_fwd_spiked_rescale():
+    """force the online-softmax rescale branch: a large score late in the key sweep."""
+    from kubeoperator_amd.ops.functional import flash_attention
+    from kubeoperator_amd.ops.reference import attention_ref
+
+    B, S, Hq, Hkv, D = 1, 512, 4, 4, 128
+    torch.manual_seed(8)
+    qkv = (0.3 * torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV)).to(torch.bfloat16)
+    a, c = Hq * D, (Hq + Hkv) * D
+    qkv[300, a:a + D] = qkv[400, :D] * 8  # key 300 aligns strongly with query 400
+    o, lse = flash_attention(qkv[:, :a], qkv[:, a:c], qkv[:, c:], B, S, Hq, Hkv, D, True)
+    o_ref, lse_ref = attention_ref(qkv[:, :a], qkv[:, a:c], qkv[:, c:], B, S, Hq, Hkv, D, True)
+    assert rel_err(o, o_ref) < 2e-2
+
+
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 8, 2), (64, 4, 4)])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_bwd(D, Hq, Hkv, causal):
+    from kubeoperator_amd.ops.functional import rope_attention
+
+    B, S = 2, 256
+    torch.manual_seed(9)
+    qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = rope_attention(qkv, None, None, B, S, Hq, Hkv, D, causal=causal, use_rope=False)
+    do = torch.randn_like(o)
+    (o.float() * do.float()).sum().backward()
+    # fp32 reference through autograd
+    x = qkv.detach().float().requires_grad_(True)
+    a, c = Hq * D, (Hq + Hkv) * D
+    qh = x[:, :a].reshape(B, S, Hq, D).transpose(1, 2)
+    kh = x[:, a:c].reshape(B, S, Hkv, D).transpose(1, 2).repeat_interleave(Hq // Hkv, 1)
+    vh = x[:, c:].reshape(B, S, Hkv, D).transpose(1, 2).repeat_interleave(Hq // Hkv, 1)
+    s = qh @ kh.transpose(-1, -2) / math.sqrt(D)
+    if causal:
+        s = s.masked_fill(torch.ones(S, S, device=DEV, dtype=torch.bool).triu(1), float("-inf"))
+    of = (torch.softmax(s, -1) @ vh).transpose(1, 2).reshape(B * S, a)
+    (of * do.float()).sum().backward()
+    assert rel_err(o, of) < 2e-2
+    g, gr = qkv.grad.float(), x.grad
+    for name, sl in (("dq", slice(0, a)), ("dk", slice(a, c)), ("dv", slice(c, None))):
+        assert rel_err(g[:, sl], gr[:, sl]) < 3e-2, name
+
+
+def test_rope_attention_end_to_end_grad():
+    from kubeoperator_amd.ops.functional import rope_attention
+    from kubeoperator_amd.ops.reference import rope_cache
+
+    B, S, Hq, Hkv, D = 1, 128, 4, 2, 128
+    cos, sin = rope_cache(S, D, 10000.0, device=DEV)
+    torch.manual_seed(10)
+    qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    o = rope_attention(qkv, cos, sin, B, S, Hq, Hkv, D)
+    do = torch.randn_like(o)
+    (o.float() * do.float()).sum().backward()
+    qc = qkv.detach().cpu().float().requires_grad_(True)
+    oc = rope_attention(qc, cos.cpu(), sin.cpu(), B, S, Hq, Hkv, D)
+    (oc * do.cpu().float()).sum().backward()
+    assert rel_err(o.cpu(), oc) < 2e-2
+    assert rel_err(qkv.grad.cpu(), qc.grad) < 3e-2

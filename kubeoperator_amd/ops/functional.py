@@ -206,9 +206,11 @@ def gelu(x):
 # ---------------------------------------------------------------------------------------------------
 class _RopeAttention(Function):
     @staticmethod
-    def forward(ctx, qkv, cos, sin, B, S, Hq, Hkv, D, causal, scale, use_rope):
+    def forward(ctx, qkv, cos, sin, B, S, Hq, Hkv, D, causal, scale, use_rope, inplace):
         lib = _lib()
         qkv = qkv.contiguous()
+        if use_rope and not inplace:
+            qkv = qkv.clone()
         if use_rope:
             lib.rope_(qkv, cos, sin, None, S, Hq + Hkv, D, False)
         q = qkv[:, : Hq * D]
@@ -235,18 +237,22 @@ class _RopeAttention(Function):
                            B, S, Hq, Hkv, D, scale, causal)
         if use_rope:
             lib.rope_(dqkv, cos, sin, None, S, Hq + Hkv, D, True)
-        return dqkv, None, None, None, None, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None, None, None, None, None
 
 
-def rope_attention(qkv, cos, sin, B, S, Hq, Hkv, D, causal=True, scale=None, use_rope=True):
-    """Fused-QKV activation [B*S, (Hq+2Hkv)*D] -> attention output [B*S, Hq*D] (RoPE on Q,K if use_rope)."""
+def rope_attention(qkv, cos, sin, B, S, Hq, Hkv, D, causal=True, scale=None, use_rope=True, inplace=True):
+    """Fused-QKV activation [B*S, (Hq+2Hkv)*D] -> attention output [B*S, Hq*D] (RoPE on Q,K if use_rope).
+
+    With ``inplace`` (the model's setting) RoPE overwrites the Q/K columns of ``qkv`` -- safe there because
+    the QKV projection's output has no other consumer -- saving one [T, (Hq+Hkv)D] copy per layer.
+    """
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if not qkv.is_cuda:
         x = ref.rope_ref(qkv, cos, sin, S, Hq + Hkv, D) if use_rope else qkv
         a, c = Hq * D, (Hq + Hkv) * D
         o, _ = _attn_ref_autograd(x[:, :a], x[:, a:c], x[:, c:], B, S, Hq, Hkv, D, causal, scale)
         return o
-    return _RopeAttention.apply(qkv, cos, sin, B, S, Hq, Hkv, D, causal, scale, use_rope)
+    return _RopeAttention.apply(qkv, cos, sin, B, S, Hq, Hkv, D, causal, scale, use_rope, inplace)
 
 
 def _attn_ref_autograd(q, k, v, B, S, Hq, Hkv, D, causal, scale):

@@ -250,7 +250,7 @@ def test_rope_attention_end_to_end_grad():
     cos, sin = rope_cache(S, D, 10000.0, device=DEV)
     torch.manual_seed(10)
     qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
-    o = rope_attention(qkv, cos, sin, B, S, Hq, Hkv, D)
+    o = rope_attention(qkv, cos, sin, B, S, Hq, Hkv, D, inplace=False)
     do = torch.randn_like(o)
     (o.float() * do.float()).sum().backward()
     qc = qkv.detach().cpu().float().requires_grad_(True)

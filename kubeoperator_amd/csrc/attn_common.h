@@ -1,0 +1,73 @@
+// Shared device helpers of the flash-attention kernels (gfx950): MFMA wrapper, LDS row / transposed reads,
+// the swizzled LDS tile image, LDS-DMA issue and the XCD-aware block remap.
+#pragma once
+#include "common.h"
+
+namespace kop {
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
+
+__device__ __forceinline__ bf16x4 lds_tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4_t*)(p));
+}
+__device__ __forceinline__ uint32_t lds_addr(const char* p) {
+  return (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const char*)(p));
+}
+// Transposed read hidden from hipcc's memory model: the builtin form makes hipcc drain every in-flight
+// LDS-DMA (vmcnt(0)) before it. The caller retires these with lds_wait_tr() before the first consumer.
+__device__ __forceinline__ bf16x4 lds_tr_read_asm(const char* p) {
+  bf16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(lds_addr(p)));
+  return r;
+}
+__device__ __forceinline__ bf16x8 lds_read8(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
+__device__ __forceinline__ bf16x8 cat44(bf16x4 a, bf16x4 b) {
+  return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// Byte offset of 16-byte chunk `ch` of row `row` in a swizzled [rows][ROWB bytes] LDS image.
+// 256-B rows: chunk ^ (((row&3)<<2)|((row>>2)&3)) serves both ds_read_b128 row reads and
+// ds_read_b64_tr_b16 transposed reads (guide T10 image (b)); 128-B rows: chunk ^ ((row>>1)&7).
+template <int ROWB>
+__device__ __forceinline__ int swz_xor(int row) {
+  if constexpr (ROWB == 256) return ((row & 3) << 2) | ((row >> 2) & 3);
+  else return (row >> 1) & 7;
+}
+template <int ROWB>
+__device__ __forceinline__ int swz(int row, int ch) {
+  return row * ROWB + 16 * (ch ^ swz_xor<ROWB>(row));
+}
+
+// One 16-B-per-lane LDS-DMA (global_load_lds_dwordx4): lane l's 16 bytes land at lds_uniform + 16*l.
+__device__ __forceinline__ void glds16(const void* g, char* lds_uniform) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_uniform, 16, 0, 0);
+}
+
+// Fill a swizzled [rows][ROWB] LDS image of `rows` rows by LDS-DMA: pieces of 1 KiB are spread over the
+// NW waves of the block; each lane's SOURCE chunk is permuted so the lane-linear destination is the
+// swizzled image (guide §5.4 rule 21). Issues (rows*ROWB/1024)/NW DMA instructions per wave.
+template <int ROWB, int NW, int ROWS>
+__device__ __forceinline__ void dma_tile(char* lds, const bf16_t* src, int64_t row_stride, int wid, int lane) {
+  constexpr int SLOTS = ROWB / 16, RPP = 1024 / ROWB;
+  constexpr int PIECES = ROWS * ROWB / 1024;
+  static_assert(PIECES % NW == 0, "tile pieces must split evenly over the waves");
+  const int prow = lane / SLOTS, pslot = lane % SLOTS;
+#pragma unroll
+  for (int i = 0; i < PIECES / NW; ++i) {
+    const int piece = wid + i * NW;
+    const int row = piece * RPP + prow;
+    const int ch = pslot ^ swz_xor<ROWB>(row);
+    glds16(src + (int64_t)row * row_stride + ch * 8, lds + piece * 1024);
+  }
+}
+
+// bijective XCD-aware remap of the linear block id (guide §5 "XCD swizzle must be bijective")
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, slot = bid >> 3;
+  const int q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+}
+
+}  // namespace kop

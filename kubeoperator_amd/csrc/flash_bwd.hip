@@ -1,0 +1,459 @@
+// Flash attention BACKWARD for gfx950 (CDNA4 / MI355X), bf16 in / fp32 accumulate, causal or full, GQA,
+// head_dim 64 or 128, on the 32x32x16 bf16 MFMA. Same tensor addressing as flash_fwd.hip.
+//
+// Why two main kernels and no dQ atomics: on MI355X float atomics execute at the memory side at
+// ~1.3 TB/s chip-wide (MI355X_MICROARCH.md "Global float atomics"). The one-kernel FA2 form adds a dQ
+// partial per (key block, query tile): at Llama-3-8B shape (S 8192, 32 heads, 128-key blocks) that is
+// 4.3 GB of atomic bytes per layer -> a 3.3 ms floor, more than all the MFMA work. Recomputing S and dP
+// in a second sweep costs 2 extra MFMA products instead, at full MFMA rate and with no cross-workgroup
+// traffic, so:
+//
+//   fa_bwd_delta_kernel : delta = rowsum(dO * O)                                   [B, Hq, S] fp32
+//   fa_bwd_dkdv_kernel  : one workgroup = 4 waves = 128 keys of one (b, q-head); sweeps the query
+//       tiles (64 rows) that see them. Key on the lane: S = Q.K^T and dP = dO.V^T with K^T / V^T
+//       operand fragments resident in VGPRs, -LSE/scale and -delta loaded as the initial accumulators
+//       (p = exp2(c*acc), no subtraction); their accumulators are directly the B operands of
+//       dV^T += dO^T.P and dK^T += Q^T.dS (transposed reads of the Q / dO tiles). Q, dO, LSE, delta
+//       tiles arrive by LDS-DMA into a 2-deep ring behind counted vmcnt + raw barriers.
+//       Writes per-q-head fp32 dK/dV partials (summed over the GQA group by the finalize kernel).
+//   fa_bwd_dq_kernel    : one workgroup = 4 waves = 128 queries of one (b, q-head); sweeps the key
+//       tiles (64 keys) like the forward pass. Query on the lane: S^T = K.Q^T and dP^T = V.dO^T with
+//       Q^T / dO^T resident, per-lane scalar LSE and delta, dS^T = P^T (dP^T - delta) packed to bf16
+//       is directly the B operand of dQ^T += K^T.dS^T (K^T by transposed reads of the K tile).
+//       dQ is written once, in bf16, straight into the strided dQKV gradient.
+//   fa_bwd_finalize_kernel : dK, dV = bf16(sum over the GQA group of the per-q-head partials).
+#include "attn_common.h"
+#include "kernels.h"
+
+namespace kop {
+
+// delta[b, h, s] = sum_d dO * O
+template <int D>
+__global__ void __launch_bounds__(256) fa_bwd_delta_kernel(const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout,
+                                                           float* __restrict__ delta, int B, int S, int Hq, int64_t os,
+                                                           int64_t dos) {
+  constexpr int LPR = D / 8;  // lanes per row
+  const int64_t rows = (int64_t)B * S * Hq;
+  const int64_t row = (int64_t)blockIdx.x * (256 / LPR) + threadIdx.x / LPR;
+  const int c = threadIdx.x % LPR;
+  float a = 0.f;
+  if (row < rows) {
+    const int64_t t = row / Hq;
+    const int h = (int)(row % Hq);
+    float x[8], y[8];
+    unpack8(*reinterpret_cast<const u32x4*>(o + t * os + h * D + c * 8), x);
+    unpack8(*reinterpret_cast<const u32x4*>(dout + t * dos + h * D + c * 8), y);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a += x[i] * y[i];
+  }
+#pragma unroll
+  for (int off = LPR / 2; off > 0; off >>= 1) a += __shfl_xor(a, off, 64);
+  if (row < rows && c == 0) {
+    const int64_t t = row / Hq;
+    const int h = (int)(row % Hq);
+    const int bb = (int)(t / S), s = (int)(t % S);
+    delta[((int64_t)(bb * Hq + h)) * S + s] = a;
+  }
+}
+
+// =============================================================================================
+// dK / dV
+// =============================================================================================
+template <int D, int NW>
+__global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
+    float* __restrict__ dk_part, float* __restrict__ dv_part, int B, int S, int Hq, int Hkv, int64_t qs, int64_t ks,
+    int64_t vs, int64_t dos, float scale, int causal) {
+  // LDS: the workgroup's K block (BN rows, read as the S = Q.K^T B operand) + a 2-deep ring of 32-query
+  // stages {Q, dO, lse/delta}; 66 KiB at D = 128 so two workgroups share a CU (V^T stays in VGPRs).
+  constexpr int BN = 32 * NW, BQ = 32, ROWB = D * 2;
+  constexpr int KB = BN * ROWB;                  // K block bytes
+  constexpr int QT = BQ * ROWB;                  // bytes of one Q (or dO) stage
+  constexpr int STAGE = 2 * QT + 1024;           // Q, dO, {lse[32], delta[32]} piece
+  constexpr int MYP = (2 * QT / 1024) / NW;      // Q/dO DMA pieces per wave per stage
+  static_assert(MYP * NW * 1024 == 2 * QT, "stage must split evenly over the waves");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const Kl = smem;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int tq = (lane & 15) >> 2, tp = lane & 3, tg1 = (lane >> 4) & 1;
+  const int nkb = S / BN;
+  const int nwork = B * Hq * nkb;
+  const int work = xcd_remap(blockIdx.x, nwork);
+  const int kb = work / (B * Hq);  // heaviest key blocks (earliest keys under a causal mask) first
+  const int rest = work % (B * Hq);
+  const int b = rest / Hq, hq = rest % Hq;
+  const int kvh = hq / (Hq / Hkv);
+  const int k0 = kb * BN, k0w = k0 + 32 * wid;
+  const float c2 = scale * 1.4426950408889634f;
+  const float lse_mul = 1.f / scale;
+
+  const float* lse_h = lse + ((int64_t)(b * Hq + hq)) * S;
+  const float* del_h = delta + ((int64_t)(b * Hq + hq)) * S;
+  const bf16_t* qbase = q + (int64_t)(b * S) * qs + hq * D;
+  const bf16_t* dobase = dout + (int64_t)(b * S) * dos + hq * D;
+  // first query tile that sees any key of this workgroup; the waves of later keys skip leading tiles
+  const int qt0 = causal ? k0 / BQ : 0;
+  const int nqt = S / BQ;
+
+  auto issue = [&](int qt, int stage) {
+    char* base = smem + KB + stage * STAGE;
+    const int q0 = qt * BQ;
+    dma_tile<ROWB, NW, BQ>(base, qbase + (int64_t)q0 * qs, qs, wid, lane);
+    dma_tile<ROWB, NW, BQ>(base + QT, dobase + (int64_t)q0 * dos, dos, wid, lane);
+    if (wid == 0) {
+      // lanes 0-7: lse[q0..q0+31], lanes 8-15: delta[...]; lanes 16-63 repeat into the unused tail
+      const int l = lane & 15;
+      const float* src = (l < 8 ? lse_h + q0 + 4 * l : del_h + q0 + 4 * (l - 8));
+      glds16(src, base + 2 * QT);
+    }
+  };
+
+  // K block of the workgroup -> LDS (counted with the first stage)
+  dma_tile<ROWB, NW, BN>(Kl, k + (int64_t)(b * S + k0) * ks + kvh * D, ks, wid, lane);
+  issue(qt0, 0);
+  // V^T operand fragments of this wave's 32 keys (B operand of dP = dO.V^T; key = k0w + r), resident
+  bf16x8 vf[D / 16];
+  {
+    const bf16_t* vp = v + (int64_t)(b * S + k0w + r) * vs + kvh * D + 8 * hh;
+#pragma unroll
+    for (int kk = 0; kk < D / 16; ++kk) vf[kk] = *reinterpret_cast<const bf16x8*>(vp + 16 * kk);
+#pragma unroll
+    for (int kk = 0; kk < D / 16; ++kk) asm volatile("" : "+v"(vf[kk]));
+  }
+  f32x16 dkacc[D / 32], dvacc[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) dkacc[i] = dvacc[i] = f32x16{0};
+
+  for (int qt = qt0; qt < nqt; ++qt) {
+    const int stage = (qt - qt0) & 1;
+    if (qt + 1 < nqt) {
+      issue(qt + 1, stage ^ 1);
+      if (wid == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MYP + 1) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MYP) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const char* Ql = smem + KB + stage * STAGE;
+    const char* Ol = Ql + QT;
+    const float* LD = reinterpret_cast<const float*>(Ql + 2 * QT);
+    const int qs0 = qt * BQ;
+    if (!causal || qs0 + 31 >= k0w) {  // else every query of the tile precedes every key of the wave
+      f32x16 sacc, dpacc;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int qr = 8 * g4 + 4 * hh;
+        const f32x4 lv = *reinterpret_cast<const f32x4*>(LD + qr);
+        const f32x4 dv = *reinterpret_cast<const f32x4*>(LD + 32 + qr);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          sacc[4 * g4 + e] = -lv[e] * lse_mul;
+          dpacc[4 * g4 + e] = -dv[e];
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < D / 16; ++kk) {
+        const bf16x8 qa = lds_read8(Ql + swz<ROWB>(r, 2 * kk + hh));
+        const bf16x8 kbf = lds_read8(Kl + swz<ROWB>(32 * wid + r, 2 * kk + hh));
+        const bf16x8 oa = lds_read8(Ol + swz<ROWB>(r, 2 * kk + hh));
+        sacc = mfma32(qa, kbf, sacc);
+        dpacc = mfma32(oa, vf[kk], dpacc);
+      }
+      const int key = k0w + r;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int qi = qs0 + (j & 3) + 8 * (j >> 2) + 4 * hh;
+        float p = __builtin_amdgcn_exp2f(sacc[j] * c2);
+        if (causal && key > qi) p = 0.f;
+        sacc[j] = p;
+        dpacc[j] = p * dpacc[j];
+      }
+      bf16x8 pb[2], sb[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          const uint32_t a = pack2(sacc[8 * s + j], sacc[8 * s + j + 1]);
+          const uint32_t c = pack2(dpacc[8 * s + j], dpacc[8 * s + j + 1]);
+          pb[s][j] = (short)(a & 0xffff);
+          pb[s][j + 1] = (short)(a >> 16);
+          sb[s][j] = (short)(c & 0xffff);
+          sb[s][j + 1] = (short)(c >> 16);
+        }
+      }
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt) {
+        const int col = dt * 32 + 16 * tg1 + 4 * tp;
+        const int ch = col >> 3, bo = (col & 7) * 2;
+        bf16x4 t[8];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int rowA = 16 * s + 4 * hh + tq;
+          t[4 * s + 0] = lds_tr_read_asm(Ol + swz<ROWB>(rowA, ch) + bo);
+          t[4 * s + 1] = lds_tr_read_asm(Ol + swz<ROWB>(rowA + 8, ch) + bo);
+          t[4 * s + 2] = lds_tr_read_asm(Ql + swz<ROWB>(rowA, ch) + bo);
+          t[4 * s + 3] = lds_tr_read_asm(Ql + swz<ROWB>(rowA + 8, ch) + bo);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]),
+                       "+v"(t[7]));
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          dvacc[dt] = mfma32(cat44(t[4 * s], t[4 * s + 1]), pb[s], dvacc[dt]);
+          dkacc[dt] = mfma32(cat44(t[4 * s + 2], t[4 * s + 3]), sb[s], dkacc[dt]);
+        }
+      }
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // stage is refilled by the next iteration's DMA
+  }
+  // per-q-head partials: lane holds dK^T[d][key = k0w + r]
+  float* dkp = dk_part + (int64_t)(b * S + k0w + r) * Hq * D + hq * D;
+  float* dvp = dv_part + (int64_t)(b * S + k0w + r) * Hq * D + hq * D;
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt) {
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = dt * 32 + 8 * g4 + 4 * hh;
+      *reinterpret_cast<f32x4*>(dkp + d) = f32x4{dkacc[dt][4 * g4] * scale, dkacc[dt][4 * g4 + 1] * scale,
+                                                 dkacc[dt][4 * g4 + 2] * scale, dkacc[dt][4 * g4 + 3] * scale};
+      *reinterpret_cast<f32x4*>(dvp + d) =
+          f32x4{dvacc[dt][4 * g4], dvacc[dt][4 * g4 + 1], dvacc[dt][4 * g4 + 2], dvacc[dt][4 * g4 + 3]};
+    }
+  }
+}
+
+// =============================================================================================
+// dQ
+// =============================================================================================
+template <int D, int NW>
+__global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dq_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
+    bf16_t* __restrict__ dq, int B, int S, int Hq, int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t dos,
+    int64_t dqs, float scale, int causal) {
+  constexpr int BM = 32 * NW, BN = 64, ROWB = D * 2;
+  constexpr int TILE = BN * ROWB;
+  constexpr int PPW = (TILE / 1024) / NW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+#define KBUF(buf) (smem + (buf) * 2 * TILE)
+#define VBUF(buf) (smem + (buf) * 2 * TILE + TILE)
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int tq = (lane & 15) >> 2, tp = lane & 3, tg1 = (lane >> 4) & 1;
+  const int nqb = S / BM;
+  const int nwork = B * Hq * nqb;
+  const int work = xcd_remap(blockIdx.x, nwork);
+  const int qb = causal ? (nqb - 1 - work / (B * Hq)) : work / (B * Hq);
+  const int rest = work % (B * Hq);
+  const int b = rest / Hq, hq = rest % Hq;
+  const int kvh = hq / (Hq / Hkv);
+  const int q0 = qb * BM, q0w = q0 + wid * 32;
+  const int ntiles = causal ? (q0 + BM) / BN : S / BN;
+  const float c2 = scale * 1.4426950408889634f;
+
+  const bf16_t* kbase = k + (int64_t)(b * S) * ks + kvh * D;
+  const bf16_t* vbase = v + (int64_t)(b * S) * vs + kvh * D;
+  auto issue = [&](int t, int buf) {
+    dma_tile<ROWB, NW, BN>(KBUF(buf), kbase + (int64_t)(t * BN) * ks, ks, wid, lane);
+    dma_tile<ROWB, NW, BN>(VBUF(buf), vbase + (int64_t)(t * BN) * vs, vs, wid, lane);
+  };
+  issue(0, 0);
+
+  const int qi = q0w + r;
+  bf16x8 qf[D / 16], of[D / 16];
+  float lse2, dl;
+  {
+    const bf16_t* qp = q + (int64_t)(b * S + qi) * qs + hq * D + 8 * hh;
+    const bf16_t* op = dout + (int64_t)(b * S + qi) * dos + hq * D + 8 * hh;
+#pragma unroll
+    for (int kk = 0; kk < D / 16; ++kk) {
+      qf[kk] = *reinterpret_cast<const bf16x8*>(qp + 16 * kk);
+      of[kk] = *reinterpret_cast<const bf16x8*>(op + 16 * kk);
+    }
+    lse2 = lse[((int64_t)(b * Hq + hq)) * S + qi] * 1.4426950408889634f;
+    dl = delta[((int64_t)(b * Hq + hq)) * S + qi];
+#pragma unroll
+    for (int kk = 0; kk < D / 16; ++kk) asm volatile("" : "+v"(qf[kk]), "+v"(of[kk]));
+    asm volatile("" : "+v"(lse2), "+v"(dl));
+  }
+  f32x16 dqacc[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) dqacc[i] = f32x16{0};
+
+  for (int it = 0; it < ntiles; ++it) {
+    const int buf = it & 1;
+    if (it + 1 < ntiles) {
+      issue(it + 1, buf ^ 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int kv0 = it * BN;
+    if (!causal || kv0 <= q0w + 31) {
+      const char* Kb = KBUF(buf);
+      const char* Vb = VBUF(buf);
+      f32x16 s0 = f32x16{0}, s1 = f32x16{0}, p0 = f32x16{0}, p1 = f32x16{0};
+#pragma unroll
+      for (int kk = 0; kk < D / 16; ++kk) {
+        const bf16x8 ka = lds_read8(Kb + swz<ROWB>(r, 2 * kk + hh));
+        const bf16x8 kb = lds_read8(Kb + swz<ROWB>(32 + r, 2 * kk + hh));
+        const bf16x8 va = lds_read8(Vb + swz<ROWB>(r, 2 * kk + hh));
+        const bf16x8 vb = lds_read8(Vb + swz<ROWB>(32 + r, 2 * kk + hh));
+        s0 = mfma32(ka, qf[kk], s0);
+        s1 = mfma32(kb, qf[kk], s1);
+        p0 = mfma32(va, of[kk], p0);
+        p1 = mfma32(vb, of[kk], p1);
+      }
+      const bool diag = causal && kv0 + BN - 1 > q0w;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int key = kv0 + (j & 3) + 8 * (j >> 2) + 4 * hh;
+        float pa = __builtin_amdgcn_exp2f(fmaf(s0[j], c2, -lse2));
+        float pb = __builtin_amdgcn_exp2f(fmaf(s1[j], c2, -lse2));
+        if (diag && key > qi) pa = 0.f;
+        if (diag && key + 32 > qi) pb = 0.f;
+        s0[j] = pa * (p0[j] - dl);
+        s1[j] = pb * (p1[j] - dl);
+      }
+      bf16x8 sf[4];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          const uint32_t a = pack2(s0[8 * s + j], s0[8 * s + j + 1]);
+          const uint32_t c = pack2(s1[8 * s + j], s1[8 * s + j + 1]);
+          sf[s][j] = (short)(a & 0xffff);
+          sf[s][j + 1] = (short)(a >> 16);
+          sf[2 + s][j] = (short)(c & 0xffff);
+          sf[2 + s][j + 1] = (short)(c >> 16);
+        }
+      }
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt) {
+        const int col = dt * 32 + 16 * tg1 + 4 * tp;
+        const int ch = col >> 3, bo = (col & 7) * 2;
+        bf16x4 t[8];
+#pragma unroll
+        for (int ks4 = 0; ks4 < 4; ++ks4) {
+          const int rowA = (ks4 >> 1) * 32 + 16 * (ks4 & 1) + 4 * hh + tq;
+          t[2 * ks4] = lds_tr_read_asm(Kb + swz<ROWB>(rowA, ch) + bo);
+          t[2 * ks4 + 1] = lds_tr_read_asm(Kb + swz<ROWB>(rowA + 8, ch) + bo);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]),
+                       "+v"(t[7]));
+#pragma unroll
+        for (int ks4 = 0; ks4 < 4; ++ks4) dqacc[dt] = mfma32(cat44(t[2 * ks4], t[2 * ks4 + 1]), sf[ks4], dqacc[dt]);
+      }
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+#undef KBUF
+#undef VBUF
+  bf16_t* dp = dq + (int64_t)(b * S + qi) * dqs + hq * D;
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt) {
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      u32x2 w;
+      w[0] = pack2(dqacc[dt][4 * g4] * scale, dqacc[dt][4 * g4 + 1] * scale);
+      w[1] = pack2(dqacc[dt][4 * g4 + 2] * scale, dqacc[dt][4 * g4 + 3] * scale);
+      *reinterpret_cast<u32x2*>(dp + dt * 32 + 8 * g4 + 4 * hh) = w;
+    }
+  }
+}
+
+// dk/dv = bf16(sum over the GQA group of the per-q-head partials)
+template <int D>
+__global__ void __launch_bounds__(256) fa_bwd_finalize_kernel(const float* __restrict__ dk_part,
+                                                              const float* __restrict__ dv_part, bf16_t* __restrict__ dk,
+                                                              bf16_t* __restrict__ dv, int64_t T, int Hq, int Hkv,
+                                                              int64_t dks, int64_t dvs) {
+  const int grp = Hq / Hkv;
+  const int64_t nk = T * Hkv * (D / 8);
+  for (int64_t it = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; it < nk; it += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = it / (Hkv * (D / 8));
+    const int rem = (int)(it % (Hkv * (D / 8)));
+    const int h = rem / (D / 8), c8 = rem % (D / 8);
+    float fk[8] = {0, 0, 0, 0, 0, 0, 0, 0}, fv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int g = 0; g < grp; ++g) {
+      const int64_t off = t * Hq * D + (int64_t)(h * grp + g) * D + c8 * 8;
+      const f32x4* pk = reinterpret_cast<const f32x4*>(dk_part + off);
+      const f32x4* pv = reinterpret_cast<const f32x4*>(dv_part + off);
+      const f32x4 k0 = pk[0], k1 = pk[1], v0 = pv[0], v1 = pv[1];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        fk[e] += k0[e];
+        fk[e + 4] += k1[e];
+        fv[e] += v0[e];
+        fv[e + 4] += v1[e];
+      }
+    }
+    *reinterpret_cast<u32x4*>(dk + t * dks + h * D + c8 * 8) = pack8(fk);
+    *reinterpret_cast<u32x4*>(dv + t * dvs + h * D + c8 * 8) = pack8(fv);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+constexpr int kBwdWaves = 4;
+
+size_t flash_attn_bwd_workspace(int B, int S, int Hq, int D) {
+  // dk_part + dv_part (fp32, [B*S, Hq, D] each) + delta [B, Hq, S]
+  return (size_t)B * S * Hq * D * 4 * 2 + (size_t)B * Hq * S * 4;
+}
+
+template <int D>
+static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
+                       const float* lse, bf16_t* dq, bf16_t* dk, bf16_t* dv, void* workspace, int B, int S, int Hq,
+                       int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t os, int64_t dos, int64_t dqs, int64_t dks,
+                       int64_t dvs, float scale, bool causal, hipStream_t stream) {
+  constexpr int NW = kBwdWaves;
+  const int64_t T = (int64_t)B * S;
+  float* dk_part = reinterpret_cast<float*>(workspace);
+  float* dv_part = dk_part + T * Hq * D;
+  float* delta = dv_part + T * Hq * D;
+  const int rows_per_block = 256 / (D / 8);
+  fa_bwd_delta_kernel<D><<<(int)((T * Hq + rows_per_block - 1) / rows_per_block), 256, 0, stream>>>(
+      o, dout, delta, B, S, Hq, os, dos);
+  const size_t lds_kv = 32 * NW * (D * 2) + 2 * (2 * 32 * (D * 2) + 1024);
+  const size_t lds_q = 4 * 64 * (D * 2);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)fa_bwd_dkdv_kernel<D, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds_kv);
+    (void)hipFuncSetAttribute((const void*)fa_bwd_dq_kernel<D, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds_q);
+    attr = true;
+  }
+  fa_bwd_dkdv_kernel<D, NW><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(
+      q, k, v, dout, lse, delta, dk_part, dv_part, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);
+  fa_bwd_dq_kernel<D, NW><<<B * Hq * (S / (32 * NW)), NW * 64, lds_q, stream>>>(
+      q, k, v, dout, lse, delta, dq, B, S, Hq, Hkv, qs, ks, vs, dos, dqs, scale, causal);
+  fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs);
+}
+
+int flash_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
+                   const float* lse, bf16_t* dq, bf16_t* dk, bf16_t* dv, void* workspace, int B, int S, int Hq,
+                   int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, int64_t dos, int64_t dqs,
+                   int64_t dks, int64_t dvs, float scale, bool causal, hipStream_t stream) {
+  if (S % (32 * kBwdWaves) != 0 || S % 64 != 0 || Hq % Hkv != 0) return -1;
+  if (D == 128)
+    launch_bwd<128>(q, k, v, o, dout, lse, dq, dk, dv, workspace, B, S, Hq, Hkv, qs, ks, vs, os, dos, dqs, dks, dvs,
+                    scale, causal, stream);
+  else if (D == 64)
+    launch_bwd<64>(q, k, v, o, dout, lse, dq, dk, dv, workspace, B, S, Hq, Hkv, qs, ks, vs, os, dos, dqs, dks, dvs,
+                   scale, causal, stream);
+  else
+    return -3;
+  return 0;
+}
+
+}  // namespace kop

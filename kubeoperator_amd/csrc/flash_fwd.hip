@@ -1,0 +1,235 @@
+// Flash attention FORWARD for gfx950 (CDNA4 / MI355X): bf16 in, fp32 accumulate, causal or full, GQA,
+// head_dim 64 or 128, on the 32x32x16 bf16 MFMA.
+//
+// q/k/v/o element (b, s, h, d) at ptr + (b*S + s) * stride + h*D + d (the fused-QKV activation's column
+// views, no transposes); lse [B, Hq, S] fp32 = natural-log sum of exp(scale * q.k).
+//
+// Structure (one workgroup = NW waves = 32*NW query rows of one (b, q-head); 64-key K/V tiles):
+//   * K/V tiles arrive by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave instruction) into a 2-deep
+//     ring: no staging registers, the DMA of tile i+1 flies during tile i's MFMAs behind a COUNTED
+//     vmcnt and raw s_barrier (a __syncthreads would drain it). The XOR-swizzled LDS image is produced
+//     by permuting each lane's SOURCE address (the DMA destination is lane-linear), so row reads
+//     (ds_read_b128) and transposed reads (ds_read_b64_tr_b16) of the image are conflict-free.
+//   * swapped scores S^T = K . Q^T: K is the MFMA A operand (LDS row reads, prefetched one k-step
+//     ahead), Q^T the B operand held in VGPRs for the whole sweep; each lane owns one query row, its 32
+//     keys are in accumulator registers -> row max = in-register max + one half-wave exchange.
+//   * P never leaves registers: the S^T accumulator packed to bf16 is directly the B operand of
+//     O^T = V^T . P^T (accumulator-as-operand identity); V^T fragments come from tr_b16 reads of the
+//     row-major V image. O^T has the query on the lane, so softmax rescales are per-lane scalars.
+//   * lazy rescale: O and l are rescaled only when a tile raises some row's max by more than 2^8
+//     (wave-uniform branch); otherwise p = exp2(s - m_ref) <= 256, exact in fp32 and fine in bf16.
+//   * causal: waves skip tiles above their diagonal; blocks are issued heaviest-first and remapped so
+//     the query heads sharing one K/V head run on one XCD (shared L2).
+//   * __launch_bounds__(256, 2): <= 256 VGPRs so two workgroups (8 waves) share a CU and one wave's
+//     softmax VALU work overlaps the other's MFMAs.
+#include "attn_common.h"
+#include "kernels.h"
+
+namespace kop {
+
+template <int D, int NW>
+__global__ void __launch_bounds__(NW * 64, 2) fa_fwd_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+                                                            const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
+                                                            float* __restrict__ lse, int B, int S, int Hq, int Hkv,
+                                                            int64_t qs, int64_t ks, int64_t vs, int64_t os,
+                                                            float scale_log2, int causal) {
+  constexpr int BM = 32 * NW, BN = 64, ROWB = D * 2;
+  constexpr int TILE = BN * ROWB;          // bytes of one K or V tile
+  constexpr int SLOTS = ROWB / 16;         // 16-B slots per row
+  constexpr int RPP = 1024 / ROWB;         // rows per 1-KiB DMA piece
+  constexpr int PPW = (TILE / 1024) / NW;  // DMA pieces per wave per tile (each of K and V)
+  static_assert(PPW * NW * 1024 == TILE, "tile must split evenly over the waves");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+#define KBUF(buf) (smem + (buf) * 2 * TILE)
+#define VBUF(buf) (smem + (buf) * 2 * TILE + TILE)
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int nqb = S / BM;
+  const int nwork = B * Hq * nqb;
+  const int work = xcd_remap(blockIdx.x, nwork);
+  const int qb = causal ? (nqb - 1 - work / (B * Hq)) : work / (B * Hq);
+  const int rest = work % (B * Hq);
+  const int b = rest / Hq, hq = rest % Hq;
+  const int kvh = hq / (Hq / Hkv);
+  const int q0 = qb * BM, q0w = q0 + wid * 32;
+  const int ntiles = causal ? (q0 + BM) / BN : S / BN;
+
+  const bf16_t* kbase = k + (int64_t)(b * S) * ks + kvh * D;
+  const bf16_t* vbase = v + (int64_t)(b * S) * vs + kvh * D;
+  // DMA lane geometry: lane -> (row within piece, slot); the slot's chunk is pre-swizzled in the source
+  const int prow = lane / SLOTS, pslot = lane % SLOTS;
+  auto issue = [&](int t, int buf) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int piece = wid * PPW + i;
+      const int row = piece * RPP + prow;
+      const int ch = pslot ^ swz_xor<ROWB>(row);
+      glds16(kbase + (int64_t)(t * BN + row) * ks + ch * 8, KBUF(buf) + piece * 1024);
+      glds16(vbase + (int64_t)(t * BN + row) * vs + ch * 8, VBUF(buf) + piece * 1024);
+    }
+  };
+
+  issue(0, 0);
+
+  // Q^T operand fragments, resident for the whole sweep
+  bf16x8 qf[D / 16];
+  {
+    const bf16_t* qp = q + (int64_t)(b * S + q0w + r) * qs + hq * D + 8 * hh;
+#pragma unroll
+    for (int kk = 0; kk < D / 16; ++kk) qf[kk] = *reinterpret_cast<const bf16x8*>(qp + 16 * kk);
+    // retire the Q loads HERE: a register still pending inside the loop would make hipcc emit
+    // vmcnt(0) at its first use every iteration, draining the in-flight K/V DMA
+#pragma unroll
+    for (int kk = 0; kk < D / 16; ++kk) asm volatile("" : "+v"(qf[kk]));
+  }
+  f32x16 oacc[D / 32];
+#pragma unroll
+  for (int i = 0; i < D / 32; ++i) oacc[i] = f32x16{0};
+  float m = -INFINITY, l = 0.f;
+  const int tq = (lane & 15) >> 2, tp = lane & 3, tg1 = (lane >> 4) & 1;
+
+  for (int it = 0; it < ntiles; ++it) {
+    const int buf = it & 1;
+    if (it + 1 < ntiles) {
+      issue(it + 1, buf ^ 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int kv0 = it * BN;
+    if (!causal || kv0 <= q0w + 31) {
+      const char* Kb = KBUF(buf);
+      const char* Vb = VBUF(buf);
+      f32x16 s0 = f32x16{0}, s1 = f32x16{0};
+      bf16x8 ka = lds_read8(Kb + swz<ROWB>(r, hh));
+      bf16x8 kb = lds_read8(Kb + swz<ROWB>(32 + r, hh));
+#pragma unroll
+      for (int kk = 0; kk < D / 16; ++kk) {
+        bf16x8 na, nb;
+        if (kk + 1 < D / 16) {
+          na = lds_read8(Kb + swz<ROWB>(r, 2 * (kk + 1) + hh));
+          nb = lds_read8(Kb + swz<ROWB>(32 + r, 2 * (kk + 1) + hh));
+        }
+        s0 = mfma32(ka, qf[kk], s0);
+        s1 = mfma32(kb, qf[kk], s1);
+        if (kk + 1 < D / 16) {
+          ka = na;
+          kb = nb;
+        }
+      }
+      if (causal && kv0 + BN - 1 > q0w) {
+        const int qi = q0w + r;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int key = kv0 + (j & 3) + 8 * (j >> 2) + 4 * hh;
+          if (key > qi) s0[j] = -INFINITY;
+          if (key + 32 > qi) s1[j] = -INFINITY;
+        }
+      }
+      float mx = fmaxf(s0[0], s1[0]);
+#pragma unroll
+      for (int j = 1; j < 16; ++j) mx = fmaxf(mx, fmaxf(s0[j], s1[j]));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mt = mx * scale_log2;
+      if (__any(mt > m + 8.f)) {
+        const float mnew = fmaxf(m, mt);
+        const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+        m = mnew;
+        l *= alpha;
+#pragma unroll
+        for (int i = 0; i < D / 32; ++i) oacc[i] *= alpha;
+      }
+      float ls = 0.f;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        s0[j] = __builtin_amdgcn_exp2f(fmaf(s0[j], scale_log2, -m));
+        s1[j] = __builtin_amdgcn_exp2f(fmaf(s1[j], scale_log2, -m));
+        ls += s0[j] + s1[j];
+      }
+      l += ls;
+      bf16x8 pf[4];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          const uint32_t a = pack2(s0[8 * s + j], s0[8 * s + j + 1]);
+          const uint32_t c = pack2(s1[8 * s + j], s1[8 * s + j + 1]);
+          pf[s][j] = (short)(a & 0xffff);
+          pf[s][j + 1] = (short)(a >> 16);
+          pf[2 + s][j] = (short)(c & 0xffff);
+          pf[2 + s][j + 1] = (short)(c >> 16);
+        }
+      }
+#pragma unroll
+      for (int dt = 0; dt < D / 32; ++dt) {
+        const int col = dt * 32 + 16 * tg1 + 4 * tp;
+        const int ch = col >> 3, bo = (col & 7) * 2;
+        bf16x4 t[8];
+#pragma unroll
+        for (int ks4 = 0; ks4 < 4; ++ks4) {
+          const int rowA = (ks4 >> 1) * 32 + 16 * (ks4 & 1) + 4 * hh + tq;
+          t[2 * ks4] = lds_tr_read_asm(Vb + swz<ROWB>(rowA, ch) + bo);
+          t[2 * ks4 + 1] = lds_tr_read_asm(Vb + swz<ROWB>(rowA + 8, ch) + bo);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]),
+                       "+v"(t[7]));
+#pragma unroll
+        for (int ks4 = 0; ks4 < 4; ++ks4) oacc[dt] = mfma32(cat44(t[2 * ks4], t[2 * ks4 + 1]), pf[ks4], oacc[dt]);
+      }
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // every wave is done with buf before iteration it+1 refills it
+  }
+#undef KBUF
+#undef VBUF
+
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = 1.f / lt;
+  if (hh == 0) lse[((int64_t)(b * Hq + hq)) * S + q0w + r] = (m + __log2f(lt)) * 0.69314718056f;
+  bf16_t* op = o + (int64_t)(b * S + q0w + r) * os + hq * D;
+#pragma unroll
+  for (int dt = 0; dt < D / 32; ++dt) {
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      u32x2 w;
+      w[0] = pack2(oacc[dt][4 * g4] * inv, oacc[dt][4 * g4 + 1] * inv);
+      w[1] = pack2(oacc[dt][4 * g4 + 2] * inv, oacc[dt][4 * g4 + 3] * inv);
+      *reinterpret_cast<u32x2*>(op + dt * 32 + 8 * g4 + 4 * hh) = w;
+    }
+  }
+}
+
+constexpr int kFwdWaves = 4;
+
+template <int D>
+static void launch_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int S, int Hq,
+                       int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t os, float sl2, bool causal,
+                       hipStream_t stream) {
+  constexpr int NW = kFwdWaves;
+  const size_t lds = 4 * 64 * (D * 2);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)fa_fwd_kernel<D, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  const int grid = B * Hq * (S / (32 * NW));
+  fa_fwd_kernel<D, NW><<<grid, NW * 64, lds, stream>>>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal);
+}
+
+int flash_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int S, int Hq,
+                   int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, float scale, bool causal,
+                   hipStream_t stream) {
+  if (S % (32 * kFwdWaves) != 0 || Hq % Hkv != 0) return -1;
+  if (qs % 8 || ks % 8 || vs % 8 || os % 8) return -2;
+  const float sl2 = scale * 1.4426950408889634f;
+  if (D == 128) launch_fwd<128>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
+  else if (D == 64) launch_fwd<64>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
+  else return -3;
+  return 0;
+}
+
+}  // namespace kop

@@ -1,0 +1,306 @@
+"""DeployExecution: the cluster lifecycle state machine (reference kubeops_api/models/deploy.py:25-337).
+
+Operations (same names and params as the reference API): ``install``, ``uninstall``, ``bigip-config``,
+``upgrade`` {package}, ``scale`` {num}, ``add-worker`` {host}, ``remove-worker`` {node},
+``backup`` {backupStorageId}, ``restore`` {clusterBackupId}, plus ``gpu-validate`` (run the rocminfo
+validation pod on every GPU worker).
+
+Per operation: cluster status while running -> after (INSTALLING -> RUNNING/ERROR, DELETING -> READY,
+UPGRADING, SCALING, BACKUP, RESTORING -> RUNNING); ``ignore_errors`` operations (scale / add / remove /
+bigip) do not put the cluster in ERROR and return it to RUNNING; step list from the plan with
+pending/running/success/error bookkeeping persisted on every transition (read by the progress
+websocket); first failing playbook stops the run; a message is sent to the message center.
+
+Added by design: one active execution per cluster (409 Conflict instead of silently marking the previous
+one FAILURE), ``params.resume`` re-runs an install from its first unfinished step (kubeasz tasks are
+idempotent), and ``timedelta`` is recorded in float seconds -- the cluster-create metric.
+"""
+from __future__ import annotations
+
+import logging
+
+from sqlalchemy import select
+
+from ..runtime import jobs
+from ..store import models as M
+from ..store.db import session_scope
+from . import clusters, context, plan
+
+log = logging.getLogger("kubeoperator.deploy")
+
+OPERATIONS = ("install", "uninstall", "bigip-config", "upgrade", "scale", "add-worker", "remove-worker", "backup",
+              "restore", "gpu-validate")
+IGNORE_ERRORS = {"bigip-config", "scale", "add-worker", "remove-worker"}
+RETURN_RUNNING = {"scale", "add-worker", "remove-worker"}
+RUNNING_STATUS = {"install": "INSTALLING", "uninstall": "DELETING", "upgrade": "UPGRADING", "scale": "SCALING",
+                  "add-worker": "SCALING", "remove-worker": "SCALING", "restore": "RESTORING", "backup": "BACKUP"}
+OPERATION_NAME = {"install": "Cluster install", "uninstall": "Cluster uninstall", "upgrade": "Cluster upgrade",
+                  "scale": "Cluster scale", "add-worker": "Cluster scale", "remove-worker": "Cluster scale",
+                  "restore": "Cluster restore", "backup": "Cluster backup", "bigip-config": "F5 BIG-IP config",
+                  "gpu-validate": "GPU validation"}
+
+
+def create(cluster_name: str, operation: str, params: dict | None = None, user: str = "",
+           run: str = "queue") -> dict:
+    """Create a DeployExecution and start it (``run``: queue | inline | none)."""
+    if operation not in OPERATIONS:
+        raise ValueError(f"unknown operation {operation!r}; one of {OPERATIONS}")
+    c = clusters.get_cluster(cluster_name)
+    params = dict(params or {})
+    with session_scope() as s:
+        busy = s.scalar(select(M.Execution).where(M.Execution.project_id == c.project_id, M.Execution.kind == "deploy",
+                                                  M.Execution.state.in_(("PENDING", "STARTED"))))
+        if busy is not None:
+            raise clusters.Conflict(f"cluster {cluster_name} is busy with {busy.operation} ({busy.id})")
+        if c.deploy_type == "AUTOMATIC" and operation in ("install", "scale"):
+            from . import cloud
+
+            need = len(clusters.list_nodes(cluster_name)) if operation == "install" else int(params.get("num", 0))
+            cloud.check_capacity(c, need)
+        steps = [dict(st, status="pending") for st in plan.operation_steps(operation)]
+        e = M.Execution(kind="deploy", project_id=c.project_id, operation=operation, params=params, steps=steps,
+                        state="PENDING", created_by=user)
+        s.add(e)
+        s.flush()
+        eid = e.id
+    if run == "queue":
+        jobs.submit("start_deploy_execution", {"execution_id": eid}, job_id=eid)
+    elif run == "inline":
+        jobs.run_inline("start_deploy_execution", {"execution_id": eid}, job_id=eid)
+    return get(eid)
+
+
+def get(execution_id: str) -> dict:
+    with session_scope() as s:
+        e = s.get(M.Execution, execution_id)
+        if e is None:
+            raise clusters.NotFound(f"execution {execution_id} not found")
+        d = e.to_dict()
+    d["progress_ws_url"] = f"/ws/progress/{execution_id}/"
+    d["log_ws_url"] = f"/ws/tasks/{execution_id}/log/"
+    return d
+
+
+def to_json(execution_id: str) -> dict:
+    """What the progress websocket pushes (reference DeployExecution.to_json)."""
+    d = get(execution_id)
+    return {"steps": d["steps"], "operation": d["operation"], "state": d["state"], "current_step": d["current_step"],
+            "timedelta": d["timedelta"]}
+
+
+class _Exec:
+    def __init__(self, eid: str, logger):
+        self.id = eid
+        self.log = logger or (lambda m: None)
+        with session_scope() as s:
+            e = s.get(M.Execution, eid)
+            self.operation, self.params, self.steps = e.operation, dict(e.params or {}), list(e.steps or [])
+            self.project_id = e.project_id
+        with session_scope() as s:
+            c = s.scalar(select(M.Cluster).where(M.Cluster.project_id == self.project_id))
+            self.cluster_name = c.name
+
+    @property
+    def cluster(self) -> M.Cluster:
+        return clusters.get_cluster(self.cluster_name)
+
+    def save(self, **fields):
+        with session_scope() as s:
+            e = s.get(M.Execution, self.id)
+            e.steps = [dict(x) for x in self.steps]
+            for k, v in fields.items():
+                setattr(e, k, v)
+
+    def set_steps(self, operation: str, drop=()):
+        self.steps = [dict(st, status="pending") for st in plan.operation_steps(operation) if st["name"] not in drop]
+        self.save()
+
+    def update_step(self, name: str, status: str):
+        for i, st in enumerate(self.steps):
+            if st["name"] == name:
+                st["status"] = status
+                self.save(current_step=i)
+
+    def run_playbooks(self, ev: dict) -> dict:
+        result = {"raw": {}, "summary": {"success": True}}
+        skip = set(self.params.get("_skip_steps", []))
+        for st in self.steps:
+            pb = st.get("playbook")
+            if not pb:
+                continue
+            if st["name"] in skip:
+                self.update_step(st["name"], "success")
+                continue
+            self.update_step(st["name"], "running")
+            self.log(f"===== step {st['name']}: playbook {plan.playbook_alias(pb)} =====")
+            r = clusters.run_playbook(self.cluster, pb, ev, logger=self.log)
+            result["summary"].update(r["summary"])
+            result["raw"] = r["raw"]
+            if not r["summary"].get("success", False):
+                self.update_step(st["name"], "error")
+                result["summary"]["success"] = False
+                return result
+            self.update_step(st["name"], "success")
+        return result
+
+
+def start(execution_id: str, logger=None) -> dict:
+    ex = _Exec(execution_id, logger)
+    t0 = M.now()
+    ex.save(state="STARTED", date_start=t0)
+    c = ex.cluster
+    ev = clusters.extra_vars(c)
+    op = ex.operation
+    result = {"raw": {}, "summary": {"success": False}}
+    ignore = op in IGNORE_ERRORS
+    try:
+        if op in RUNNING_STATUS:
+            clusters.change_status(c.id, RUNNING_STATUS[op])
+        result = _dispatch(ex, c, ev)
+        ok = result.get("summary", {}).get("success", False)
+        after = {"uninstall": "READY"}.get(op, "RUNNING")
+        if ok or ignore:
+            if op not in ("bigip-config", "gpu-validate") or c.status in RUNNING_STATUS.values():
+                clusters.change_status(c.id, after)
+        else:
+            clusters.change_status(c.id, "ERROR")
+    except Exception as e:  # noqa: BLE001 - recorded on the execution and the cluster
+        log.exception("execution %s failed", execution_id)
+        ex.log(f"ERROR: {type(e).__name__}: {e}")
+        for st in ex.steps:
+            if st.get("status") == "running":
+                st["status"] = "error"
+        clusters.change_status(c.id, "ERROR")
+        result = {"raw": {}, "summary": {"success": False, "error": f"{type(e).__name__}: {e}"}}
+    ok = bool(result.get("summary", {}).get("success", False))
+    t1 = M.now()
+    ex.save(state="SUCCESS" if ok else "FAILURE", date_end=t1, timedelta=(t1 - t0).total_seconds(),
+            result_summary=clusters._jsonable(result.get("summary", {})),
+            result_raw=clusters._jsonable({k: v for k, v in (result.get("raw") or {}).items() if k != "ok"}))
+    _notify(c, op, ok)
+    return {"success": ok, "timedelta": (t1 - t0).total_seconds()}
+
+
+def _dispatch(ex: _Exec, c: M.Cluster, ev: dict) -> dict:
+    op = ex.operation
+    if op == "install":
+        drop = () if c.deploy_type == "AUTOMATIC" else ("create-resource",)
+        ex.set_steps("install", drop)
+        if ex.params.get("resume"):
+            ex.params["_skip_steps"] = _resume_skips(ex)
+        if c.deploy_type == "AUTOMATIC":
+            from . import cloud
+
+            ex.update_step("create-resource", "running")
+            cloud.create_resources(c.name, logger=ex.log)
+            ex.update_step("create-resource", "success")
+            ev.update(clusters.get_cluster(c.name).configs)
+        return ex.run_playbooks(ev)
+    if op == "uninstall":
+        ex.set_steps("uninstall")
+        if c.deploy_type == "AUTOMATIC":
+            from . import cloud
+
+            ex.update_step("uninstall", "running")
+            cloud.destroy_resources(c.name, logger=ex.log)
+            ex.update_step("uninstall", "success")
+            return {"raw": {}, "summary": {"success": True}}
+        return ex.run_playbooks(ev)
+    if op == "bigip-config":
+        ex.set_steps("bigip-config")
+        return ex.run_playbooks(ev)
+    if op == "upgrade":
+        from . import packages
+
+        name = ex.params.get("package")
+        meta = packages.get_package(name)["meta"]
+        ev.update(meta.get("vars", {}))
+        ex.set_steps("upgrade")
+        res = ex.run_playbooks(ev)
+        if res["summary"].get("success"):
+            packages.upgrade_cluster_package(c.name, name)
+        return res
+    if op == "scale":
+        ex.set_steps("scale", () if c.deploy_type == "AUTOMATIC" else ("create-resource",))
+        if c.deploy_type == "AUTOMATIC":
+            from . import cloud
+
+            ex.update_step("create-resource", "running")
+            cloud.scale_to(c.name, int(ex.params.get("num", 0)), logger=ex.log)
+            ex.update_step("create-resource", "success")
+        res = ex.run_playbooks(ev)
+        clusters.exit_new_node(c.name)
+        return res
+    if op == "add-worker":
+        ex.set_steps("add-worker")
+        hosts = ex.params.get("host") or ex.params.get("hosts")
+        for h in hosts if isinstance(hosts, list) else [hosts]:
+            clusters.add_worker(c.name, h)
+        res = ex.run_playbooks(ev)
+        clusters.exit_new_node(c.name)
+        return res
+    if op == "remove-worker":
+        ex.set_steps("remove-worker")
+        node = ex.params.get("node")
+        clusters.set_node_groups(c.name, node, ["new_node", "worker"])
+        res = ex.run_playbooks(ev)
+        if res["summary"].get("success"):
+            clusters.remove_node_record(c.name, node)
+        else:
+            clusters.exit_new_node(c.name)
+        return res
+    if op == "backup":
+        from . import backup
+
+        ex.set_steps("backup")
+        res = ex.run_playbooks(ev)
+        if res["summary"].get("success"):
+            backup.upload_backup(c.name, ex.params.get("backupStorageId"), logger=ex.log)
+        return res
+    if op == "restore":
+        from . import backup
+
+        ex.set_steps("restore")
+        backup.download_backup(c.name, ex.params.get("clusterBackupId"), logger=ex.log)
+        return ex.run_playbooks(ev)
+    if op == "gpu-validate":
+        ex.set_steps("gpu-validate")
+        return ex.run_playbooks(ev)
+    raise ValueError(op)
+
+
+def _resume_skips(ex: _Exec) -> list[str]:
+    with session_scope() as s:
+        prev = s.scalar(select(M.Execution).where(M.Execution.project_id == ex.project_id,
+                                                  M.Execution.kind == "deploy", M.Execution.operation == ex.operation,
+                                                  M.Execution.id != ex.id, M.Execution.state == "FAILURE")
+                        .order_by(M.Execution.date_created.desc()).limit(1))
+        if prev is None:
+            return []
+        return [st["name"] for st in prev.steps or [] if st.get("status") == "success"]
+
+
+def _notify(c: M.Cluster, op: str, ok: bool) -> None:
+    from . import messages
+
+    try:
+        messages.insert_message({
+            "title": OPERATION_NAME.get(op, op), "level": "INFO" if ok else "WARNING", "type": "CLUSTER",
+            "item_id": _item_of(c.id),
+            "content": {"resource": "cluster", "resource_name": c.name, "resource_type": "CLUSTER",
+                        "detail": {"message": f"{OPERATION_NAME.get(op, op)} {'succeeded' if ok else 'failed'}"},
+                        "status": clusters.get_cluster(c.name).status}})
+    except Exception:  # noqa: BLE001 - notification failure never fails the execution
+        log.exception("message insert failed")
+
+
+def _item_of(cluster_id: str):
+    with session_scope() as s:
+        r = s.scalar(select(M.ItemResource).where(M.ItemResource.resource_id == cluster_id,
+                                                  M.ItemResource.resource_type == "CLUSTER"))
+        return r.item_id if r else None
+
+
+@jobs.task("start_deploy_execution")
+def _job_start_deploy(job_id, logger, execution_id):
+    return start(execution_id, logger=logger)

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import copy
 import fnmatch
+import re
 from dataclasses import dataclass, field
 
 import yaml
@@ -159,7 +160,7 @@ class Inventory:
         if pattern in ("", "all", "*"):
             return list(self.hosts)
         result: list[str] = []
-        for raw in [p for p in pattern.replace(",", ":").split(":") if p]:
+        for raw in [p for p in re.split(r"[:,](?![^\[]*\])", pattern) if p]:
             op = ""
             if raw[0] in "&!":
                 op, raw = raw[0], raw[1:]
@@ -174,6 +175,14 @@ class Inventory:
         return sorted(result, key=lambda h: order.index(h) if h in order else 1 << 30)
 
     def _atom(self, a: str) -> list[str]:
+        m = re.match(r"^(.+)\[(-?\d*)(?::(-?\d*))?\]$", a)
+        if m:  # group[i] / group[i:j] subscripts (e.g. kube-master[0])
+            hosts = self._atom(m.group(1))
+            i = int(m.group(2)) if m.group(2) not in ("", None) else None
+            if m.group(3) is None and ":" not in a:
+                return hosts[i:i + 1] if i is not None and -len(hosts) <= i < len(hosts) else []
+            j = int(m.group(3)) if m.group(3) not in ("", None) else None
+            return hosts[i:j]
         if a in self.groups:
             return self.group_hosts(a)
         if a in self.hosts:

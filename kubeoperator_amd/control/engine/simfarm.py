@@ -1,0 +1,152 @@
+"""A simulated host farm for CPU-only plumbing runs (BASELINE config #1) and the test-suite.
+
+``SimFarm`` is a :class:`FakeTransport` pre-loaded with rules that answer the commands the provisioning
+roles issue the way real Ubuntu 22.04 nodes with kubeadm / containerd / ROCm would: kubeadm init creates
+``admin.conf`` (stateful, so re-runs are idempotent), join commands are printed, nodes report Ready,
+GPU nodes expose 8 x AMD Instinct MI355X over lspci / kfd topology / rocminfo and ``amd.com/gpu: 8``,
+validation pods succeed, etcd snapshots produce an archive that ``fetch`` can pull. Every command is
+recorded, so tests assert on the exact command stream; fault injection comes from FakeTransport
+(``unreachable``, ``fail_after``, extra rules inserted first).
+"""
+from __future__ import annotations
+
+import time
+
+from .transport import CmdResult, FakeTransport
+
+MI355X_LSPCI = "\n".join(
+    f"{b:02x}:00.0 Processing accelerators [1200]: Advanced Micro Devices, Inc. [AMD/ATI] Device [1002:75a3]"
+    for b in (0x05, 0x15, 0x65, 0x75, 0x85, 0x95, 0xe5, 0xf5))
+KUBECONFIG = """apiVersion: v1
+kind: Config
+clusters:
+- cluster: {server: 'https://%s:6443', insecure-skip-tls-verify: true}
+  name: kubernetes
+contexts:
+- context: {cluster: kubernetes, user: kubernetes-admin}
+  name: kubernetes-admin@kubernetes
+current-context: kubernetes-admin@kubernetes
+users:
+- name: kubernetes-admin
+  user: {token: sim-admin-token}
+"""
+
+
+class SimFarm(FakeTransport):
+    def __init__(self, gpu_hosts: set | None = None, gpus_per_host: int = 8, latency_s: float = 0.0):
+        super().__init__(latency_s=latency_s)
+        self.gpu_hosts = set(gpu_hosts or ())  # inventory names or addresses of the GPU machines
+        self._addr: dict[str, str] = {}
+        self.gpus_per_host = gpus_per_host
+        self._install_rules()
+
+    BASE_FILES = {
+        "/etc/ssh/sshd_config": b"#UseDNS yes\nPermitRootLogin yes\n",
+        "/etc/hosts": b"127.0.0.1 localhost\n",
+        "/etc/resolv.conf": b"nameserver 127.0.0.53\n",
+        "/etc/fstab": b"UUID=0 / ext4 defaults 0 1\n",
+        "/etc/exports": b"",
+    }
+
+    def _seed(self, host: str) -> dict:
+        fs = self.fs.setdefault(host, {})
+        if "/etc/hosts" not in fs:
+            fs.update(self.BASE_FILES)
+        return fs
+
+    def is_gpu(self, host: str) -> bool:
+        return host in self.gpu_hosts or self._addr.get(host) in self.gpu_hosts
+
+    def run(self, conn, cmd, timeout=3600, env=None, stdin=None):
+        self._addr[conn.name] = conn.address
+        self._seed(conn.name)
+        return super().run(conn, cmd, timeout, env, stdin)
+
+    def get(self, conn, src):
+        self._seed(conn.name)
+        return super().get(conn, src)
+
+    def _n_gpu_nodes(self) -> int:
+        """GPU hosts that are currently cluster members (joined and not reset)."""
+        return sum(1 for h, fs in self.fs.items() if self.is_gpu(h) and "/etc/kubernetes/kubelet.conf" in fs)
+
+    def _install_rules(self):
+        R = self.add_rule
+
+        def stat(host, cmd, fs):
+            path = cmd.split("stat -c '%F|%s|%a|%U|%Y' ", 1)[1].split(" ")[0].strip("'\"")
+            if path in fs:
+                return 0, f"regular file|{len(fs[path])}|600|root|{int(time.time())}", ""
+            return 1, "", ""
+
+        def kinit(host, cmd, fs):
+            fs["/etc/kubernetes/admin.conf"] = (KUBECONFIG % host).encode()
+            fs["/etc/kubernetes/kubelet.conf"] = b"kubelet"
+            return 0, "Your Kubernetes control-plane has initialized successfully!", ""
+
+        def kjoin(host, cmd, fs):
+            fs["/etc/kubernetes/kubelet.conf"] = b"kubelet"
+            if "--control-plane" in cmd:
+                fs["/etc/kubernetes/admin.conf"] = (KUBECONFIG % host).encode()
+            return 0, "This node has joined the cluster", ""
+
+        def reset(host, cmd, fs):
+            for p in list(fs):
+                if p.startswith("/etc/kubernetes/"):
+                    del fs[p]
+            return 0, "", ""
+
+        def cat_conf(host, cmd, fs):
+            data = fs.get("/etc/kubernetes/admin.conf")
+            return (0, data.decode(), "") if data else (1, "", "No such file")
+
+        def gpu_probe(host, cmd, fs):
+            return 0, (MI355X_LSPCI + "\n--amd-smi--\n") if self.is_gpu(host) else "--amd-smi--\n", ""
+
+        def snapshot_zip(host, cmd, fs):
+            fs["/opt/kubeoperator/backup/cluster-backup.zip"] = b"PK\x05\x06" + b"\x00" * 18
+            return 0, "", ""
+
+        # order: later add_rule calls win (inserted first), so generic rules go first
+        R(r"stat -c", fn=stat)
+        R(r"ctr version", stdout="ready")
+        R(r"kubectl get --raw=/readyz", stdout="ok")
+        R(r"kubeadm init phase upload-certs|--print-join-command.*--control-plane", stdout=(
+            "kubeadm join 127.0.0.1:6443 --token sim.token --discovery-token-ca-cert-hash sha256:00 --control-plane "
+            "--certificate-key 00"))
+        R(r"^kubeadm token create --print-join-command$",
+          stdout="kubeadm join 10.0.0.1:6443 --token sim.token --discovery-token-ca-cert-hash sha256:00")
+        R(r"^echo \$\(kubeadm token create", stdout=(
+            "kubeadm join 10.0.0.1:6443 --token sim.token --discovery-token-ca-cert-hash sha256:00 --control-plane "
+            "--certificate-key 00"))
+        R(r"^kubeadm init --config", fn=kinit)
+        R(r"^kubeadm join", fn=kjoin)
+        R(r"kubeadm reset", fn=reset)
+        R(r"kubectl get node (\S+) --no-headers",
+          fn=lambda h, c, fs: (0, f"{c.split('get node ')[1].split()[0]} Ready worker 1m v1.30.6", ""))
+        R(r"kube-flannel get pods .* wc -l", stdout="0")
+        R(r"calico-node -o jsonpath", stdout="2/2")
+        R(r"deploy coredns -o jsonpath", stdout="2")
+        R(r"deploy chartmuseum -o jsonpath", stdout="1")
+        R(r"test-sc-pod -o jsonpath", stdout="Succeeded")
+        R(r"awk '\$2 != \"Ready\"' \| wc -l", stdout="0")
+        R(r"/sys/class/kfd/kfd/topology", fn=lambda h, c, fs: (0, str(self.gpus_per_host if self.is_gpu(h) else 0), ""))
+        R(r"rocminfo \| grep -c", fn=lambda h, c, fs: (0, str(self.gpus_per_host if self.is_gpu(h) else 0), ""))
+        R(r"allocatable\.amd", fn=lambda h, c, fs: (0, " ".join([str(self.gpus_per_host)] * self._n_gpu_nodes()) + " ", ""))
+        R(r"app=rocminfo-validate -o jsonpath", fn=lambda h, c, fs: (0, "Succeeded " * self._n_gpu_nodes(), ""))
+        R(r"kubectl -n kube-system logs", stdout="Marketing Name: AMD Instinct MI355X\n  Name: gfx950")
+        R(r"lspci -nn -d 1002:", fn=gpu_probe)
+        R(r"cat /etc/kubernetes/admin.conf", fn=cat_conf)
+        R(r"date \+%s", fn=lambda h, c, fs: (0, str(int(time.time())), ""))
+        R(r"create token kubeoperator-admin", stdout="sim-sa-token")
+        R(r"zip -qr cluster-backup.zip", fn=snapshot_zip)
+        R(r"^hostname$", fn=lambda h, c, fs: (0, h, ""))
+        R(r"helm version", stdout="v3.15.4+g0")
+        R(r"systemctl is-active", rc=3)
+
+    def is_sim(self) -> bool:
+        return True
+
+
+def sim_result(rc: int = 0, stdout: str = "") -> CmdResult:
+    return CmdResult(rc, stdout, "")

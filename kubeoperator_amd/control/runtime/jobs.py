@@ -1,0 +1,193 @@
+"""Durable job runtime: queue in the store, worker threads, per-job log files, crash recovery.
+
+Replaces Celery worker + Redis broker + result backend (reference core/kubeops.py:143-194,
+celery_api/*). A job row is claimed atomically (``UPDATE ... WHERE state='PENDING'``), so any number of
+worker processes can share one store; ``WORKER_CONCURRENCY`` threads per process (reference: prefork
+``-c 4``). Each job's log goes to ``<DATA_DIR>/celery/<id[0]>/<id[1]>/<id>.log`` -- the reference's path
+convention (celery_api/utils.py:212-217) -- which the log API / websocket tail.
+
+Recovery: at worker start every job left STARTED by a dead worker is marked FAILURE (and its
+execution too), instead of the reference's "mark the previous STARTED execution FAILURE when a new one
+starts" (kubeops_api/api.py:244-248).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import socket
+import threading
+import time
+import traceback
+import uuid
+
+from sqlalchemy import select, update
+
+from ..store import models as M
+from ..store.db import session_scope
+
+log = logging.getLogger("kubeoperator.runtime")
+
+_TASKS: dict[str, callable] = {}
+
+
+def task(name: str):
+    """Register a job function ``fn(job_id, logger, **args) -> dict``."""
+    def deco(fn):
+        _TASKS[name] = fn
+        fn.task_name = name
+        return fn
+    return deco
+
+
+def registered_tasks() -> list[str]:
+    return sorted(_TASKS)
+
+
+def log_path(job_id: str) -> str:
+    from ..conf import get_config
+
+    d = os.path.join(get_config().data_dir, "celery", job_id[0], job_id[1])
+    os.makedirs(d, exist_ok=True)
+    return os.path.join(d, f"{job_id}.log")
+
+
+class JobLogger:
+    """Line logger bound to one job's log file (also the engine's display callback)."""
+
+    def __init__(self, path: str):
+        self.path = path
+        self._f = open(path, "a", buffering=1)
+        self._lock = threading.Lock()
+
+    def __call__(self, msg: str) -> None:
+        self.write(msg)
+
+    def write(self, msg: str) -> None:
+        with self._lock:
+            self._f.write(msg if msg.endswith("\n") else msg + "\n")
+            self._f.flush()
+
+    def info(self, msg: str) -> None:
+        self.write(f"{time.strftime('%Y-%m-%d %H:%M:%S')} {msg}")
+
+    def close(self):
+        with self._lock:
+            self._f.close()
+
+
+def tail(path: str, offset: int = 0, limit: int = 4096) -> tuple[str, int]:
+    """Read up to ``limit`` bytes of a log from ``offset`` (reference LogTailApi / ws.py: 4 KiB chunks)."""
+    if not os.path.exists(path):
+        return "", offset
+    with open(path, "rb") as f:
+        f.seek(offset)
+        data = f.read(limit)
+    return data.decode(errors="replace"), offset + len(data)
+
+
+def submit(name: str, args: dict | None = None, job_id: str | None = None) -> str:
+    if name not in _TASKS:
+        raise KeyError(f"unknown task {name!r}")
+    jid = job_id or str(uuid.uuid4())
+    with session_scope() as s:
+        s.add(M.Job(id=jid, name=name, args=args or {}, state="PENDING", log_path=log_path(jid)))
+    _wake.set()
+    return jid
+
+
+def get(job_id: str) -> M.Job | None:
+    with session_scope() as s:
+        return s.get(M.Job, job_id)
+
+
+def _claim(worker: str) -> M.Job | None:
+    with session_scope() as s:
+        for j in s.scalars(select(M.Job).where(M.Job.state == "PENDING").order_by(M.Job.date_created).limit(8)):
+            n = s.execute(update(M.Job).where(M.Job.id == j.id, M.Job.state == "PENDING")
+                          .values(state="STARTED", worker=worker, date_start=M.now(), attempts=j.attempts + 1)).rowcount
+            if n == 1:
+                s.flush()
+                return s.get(M.Job, j.id)
+    return None
+
+
+def run_job(job: M.Job) -> dict:
+    fn = _TASKS[job.name]
+    lg = JobLogger(job.log_path or log_path(job.id))
+    lg.info(f"Start task: {job.name} {job.id}")
+    state, result = "SUCCESS", {}
+    try:
+        out = fn(job.id, lg, **(job.args or {}))
+        result = out if isinstance(out, dict) else {"result": out}
+    except Exception as e:  # noqa: BLE001 - a job failure is data, not a crash
+        state = "FAILURE"
+        result = {"error": f"{type(e).__name__}: {e}"}
+        lg.write(traceback.format_exc())
+    lg.info(f"Task finish: {state}")
+    lg.close()
+    with session_scope() as s:
+        s.execute(update(M.Job).where(M.Job.id == job.id).values(state=state, result=result, date_end=M.now()))
+    return {"state": state, "result": result}
+
+
+def run_inline(name: str, args: dict | None = None, job_id: str | None = None) -> dict:
+    """Submit and execute in the calling thread (tests, CLI, single-process mode)."""
+    jid = submit(name, args, job_id)
+    job = _claim_specific(jid)
+    return {"id": jid, **run_job(job)}
+
+
+def _claim_specific(jid: str) -> M.Job:
+    with session_scope() as s:
+        s.execute(update(M.Job).where(M.Job.id == jid).values(state="STARTED", worker="inline", date_start=M.now()))
+        return s.get(M.Job, jid)
+
+
+def recover_orphans() -> int:
+    """Mark jobs/executions left STARTED by a dead worker as FAILURE; returns how many."""
+    with session_scope() as s:
+        n = s.execute(update(M.Job).where(M.Job.state == "STARTED")
+                      .values(state="FAILURE", result={"error": "worker died"}, date_end=M.now())).rowcount
+        s.execute(update(M.Execution).where(M.Execution.state == "STARTED")
+                  .values(state="FAILURE", date_end=M.now(), result_summary={"error": "worker died"}))
+    return n
+
+
+_wake = threading.Event()
+
+
+class WorkerPool:
+    def __init__(self, concurrency: int | None = None, poll_s: float = 1.0):
+        from ..conf import get_config
+
+        self.concurrency = concurrency or int(get_config()["WORKER_CONCURRENCY"])
+        self.poll_s = poll_s
+        self.name = f"{socket.gethostname()}:{os.getpid()}"
+        self._stop = threading.Event()
+        self._threads: list[threading.Thread] = []
+
+    def start(self, recover: bool = True):
+        if recover:
+            n = recover_orphans()
+            if n:
+                log.warning("recovered %d orphaned jobs", n)
+        for i in range(self.concurrency):
+            t = threading.Thread(target=self._loop, name=f"kop-worker-{i}", daemon=True)
+            t.start()
+            self._threads.append(t)
+        return self
+
+    def _loop(self):
+        while not self._stop.is_set():
+            job = _claim(self.name)
+            if job is None:
+                _wake.wait(self.poll_s)
+                _wake.clear()
+                continue
+            run_job(job)
+
+    def stop(self, timeout: float = 5.0):
+        self._stop.set()
+        _wake.set()
+        for t in self._threads:
+            t.join(timeout)

@@ -1,0 +1,77 @@
+"""Training entry point of the bundled chart: ``torchrun --nproc-per-node=8 -m kubeoperator_amd.train.cli``.
+
+Logs one JSON line per ``--log-every`` steps on rank 0 (step, loss, grad norm, lr, step time, tokens/s,
+TFLOP/s per GPU); checkpoints every ``--ckpt-every`` steps and resumes from the newest complete
+checkpoint with ``--resume`` (elastic restarts via ``torchrun --max-restarts`` then continue where the
+failed attempt left off).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3_8b")
+    ap.add_argument("--seq", type=int, default=8192)
+    ap.add_argument("--mbs", type=int, default=1)
+    ap.add_argument("--accum", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5, help="LR warmup steps")
+    ap.add_argument("--lr", type=float, default=3e-4)
+    ap.add_argument("--dp", default="allreduce", choices=["allreduce", "zero1"])
+    ap.add_argument("--bucket-mb", type=int, default=512)
+    ap.add_argument("--data", default="synthetic", help="'synthetic' or a flat uint16 token file")
+    ap.add_argument("--ckpt-dir", default="")
+    ap.add_argument("--ckpt-every", type=int, default=0)
+    ap.add_argument("--resume", action="store_true")
+    ap.add_argument("--log-every", type=int, default=1)
+    ap.add_argument("--device", default="auto")
+    a = ap.parse_args(argv)
+
+    import torch
+
+    from ..parallel.dist import all_reduce_max, init_distributed, shutdown
+    from . import checkpoint
+    from .data import SyntheticTokens, TokenFileDataset
+    from .trainer import TrainConfig, Trainer, lr_at
+
+    info = init_distributed(a.device)
+    tc = TrainConfig(model=a.model, micro_batch=a.mbs, seq_len=a.seq, grad_accum=a.accum, lr=a.lr,
+                     warmup_steps=a.warmup, total_steps=a.steps, dp_mode=a.dp, bucket_mb=a.bucket_mb)
+    tr = Trainer(tc, info)
+    if a.resume and a.ckpt_dir:
+        s = checkpoint.load(tr, a.ckpt_dir, info)
+        if s is not None and info.is_main:
+            print(json.dumps({"event": "resumed", "step": s}), flush=True)
+    if a.data == "synthetic":
+        data = SyntheticTokens(tr.cfg.vocab_size, a.mbs, a.seq, info.device, seed=tc.seed + tr.step, rank=info.rank)
+    else:
+        data = TokenFileDataset(a.data, a.mbs, a.seq, info.device, seed=tc.seed + tr.step, rank=info.rank,
+                                world=info.world)
+    cuda = info.device.type == "cuda"
+    flops_tok = tr.cfg.flops_per_token(a.seq)
+    while tr.step < a.steps:
+        t0 = time.perf_counter()
+        loss = tr.train_step(data.batches(a.accum))
+        if tr.step % a.log_every == 0:
+            if cuda:
+                torch.cuda.synchronize()
+            dt = all_reduce_max(time.perf_counter() - t0, info)
+            toks = info.world * tr.tokens_per_step / dt
+            if info.is_main:
+                print(json.dumps({"step": tr.step, "loss": round(float(loss), 4),
+                                  "grad_norm": round(float(tr.opt.last_grad_norm), 4),
+                                  "lr": lr_at(tr.step - 1, tc), "step_s": round(dt, 4), "tokens_per_s": round(toks, 1),
+                                  "tflops_per_gpu": round(flops_tok * toks / info.world / 1e12, 1)}), flush=True)
+        if a.ckpt_dir and a.ckpt_every and tr.step % a.ckpt_every == 0:
+            checkpoint.save(tr, a.ckpt_dir, info)
+    shutdown(info)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -287,6 +287,9 @@ def extra_vars(c: M.Cluster) -> dict:
     ev.update(context.get_settings())
     ev.update(c.configs or {})
     ev.setdefault("base_dir", "/etc/kubeoperator")
+    from ..conf import get_config
+
+    ev["controller_fetch_dir"] = os.path.join(get_config().data_dir, "fetch", c.name)
     return ev
 
 

@@ -1,0 +1,141 @@
+"""Cluster lifecycle on simulated hosts (SimFarm): register hosts with GPU discovery, create a cluster
+from a plan template, install -> gpu-validate -> add-worker -> upgrade -> backup -> restore ->
+remove-worker -> uninstall, plus failure / resume / busy-lock paths. Mirrors the reference's deploy
+state machine (kubeops_api/models/deploy.py:55-230) and its per-step status tracking."""
+import os
+
+import pytest
+
+from kubeoperator_amd.control.domain import clusters, deploy, hosts
+from kubeoperator_amd.control.store import models as M
+from kubeoperator_amd.control.store.db import session_scope
+
+
+def _cluster(template="single-master", name="demo", workers=("w1",)):
+    for hn, ip in (("m1", "10.0.0.1"), ("m2", "10.0.0.4"), ("m3", "10.0.0.5"), ("w1", "10.0.0.2"),
+                   ("w2", "10.0.0.3")):
+        try:
+            hosts.create_host({"name": hn, "ip": ip, "password": "pw"})
+        except Exception:
+            pass
+    clusters.create_cluster({"name": name, "template": template, "network_plugin": "flannel",
+                             "persistent_storage": "local-volume"})
+    masters = ["m1"] if template == "single-master" else ["m1", "m2", "m3"]
+    for m in masters:
+        clusters.add_node(name, {"name": m, "host": m, "roles": ["master"]})
+    for w in workers:
+        clusters.add_node(name, {"name": w, "host": w, "roles": ["worker"]})
+
+
+def test_host_gpu_discovery(control):
+    h = hosts.create_host({"name": "w1", "ip": "10.0.0.2", "password": "pw"})
+    assert h["status"] == "RUNNING"
+    assert h["gpu_num"] == 8 and h["gpu_info"] == "AMD Instinct MI355X"
+    c = hosts.create_host({"name": "m1", "ip": "10.0.0.1", "password": "pw"})
+    assert c["gpu_num"] == 0
+
+
+def test_lspci_parsing():
+    text = "\n".join([
+        "05:00.0 Processing accelerators [1200]: Advanced Micro Devices, Inc. [AMD/ATI] Device [1002:75a3]",
+        "15:00.0 Processing accelerators [1200]: Advanced Micro Devices, Inc. [AMD/ATI] Device [1002:74a1]",
+        "65:00.0 VGA compatible controller [0300]: ASPEED Technology, Inc. ASPEED Graphics Family [1a03:2000]",
+    ])
+    gpus = hosts.parse_lspci_amd(text)
+    names = [g["name"] for g in gpus]
+    assert names == ["AMD Instinct MI355X", "AMD Instinct MI300X"]
+
+
+def test_full_lifecycle(control):
+    _cluster()
+    e = deploy.create("demo", "install", run="inline")
+    assert e["state"] == "SUCCESS", e["result_summary"].get("dark")
+    assert [s["status"] for s in e["steps"]] == ["success"] * len(e["steps"])
+    assert clusters.get_cluster("demo").status == "RUNNING"
+    farm = control.farm
+    assert any(c.startswith("kubeadm init --config") for c in farm.commands("m1"))
+    assert any(c.startswith("kubeadm join") for c in farm.commands("w1"))
+    # GPU stack only on GPU nodes
+    assert any("amdgpu" in c for c in farm.commands("w1"))
+    assert not any("amdgpu-dkms" in c for c in farm.commands("m1"))
+    assert "apiVersion" in clusters.fetch_kubeconfig("demo")
+
+    assert deploy.create("demo", "gpu-validate", run="inline")["state"] == "SUCCESS"
+
+    e = deploy.create("demo", "add-worker", {"host": "w2"}, run="inline")
+    assert e["state"] == "SUCCESS", e["result_summary"].get("dark")
+    assert len(clusters.list_nodes("demo")) == 3
+
+    e = deploy.create("demo", "upgrade", {"package": "mi355x-k8s-next"}, run="inline")
+    assert e["state"] == "SUCCESS", e["result_summary"].get("dark")
+    c = clusters.get_cluster("demo")
+    assert c.package == "mi355x-k8s-next" and c.configs["kube_version"] == "v1.31.2"
+
+    with session_scope() as s:
+        st = M.BackupStorage(name="local", type="LOCAL", credentials={"path": str(control.tmp / "bk")})
+        s.add(st)
+        s.flush()
+        sid = st.id
+    e = deploy.create("demo", "backup", {"backupStorageId": sid}, run="inline")
+    assert e["state"] == "SUCCESS", e["result_summary"].get("dark")
+    with session_scope() as s:
+        b = s.query(M.ClusterBackup).one()
+        bid = b.id
+    assert os.listdir(control.tmp / "bk" / "demo")
+    e = deploy.create("demo", "restore", {"clusterBackupId": bid}, run="inline")
+    assert e["state"] == "SUCCESS", e["result_summary"].get("dark")
+
+    names = [n["name"] for n in clusters.list_nodes("demo")]
+    node = [n for n in names if n not in ("m1", "w1")][0]
+    e = deploy.create("demo", "remove-worker", {"node": node}, run="inline")
+    assert e["state"] == "SUCCESS"
+    assert len(clusters.list_nodes("demo")) == 2
+
+    e = deploy.create("demo", "uninstall", run="inline")
+    assert e["state"] == "SUCCESS"
+    assert clusters.get_cluster("demo").status == "READY"
+    assert "/etc/kubernetes/admin.conf" not in farm.fs["m1"]
+
+
+def test_multi_master_install(control):
+    _cluster(template="multiple-master", name="ha")
+    e = deploy.create("ha", "install", run="inline")
+    assert e["state"] == "SUCCESS", e["result_summary"].get("dark")
+    joins = [h for h in ("m2", "m3") if any("--control-plane" in c for c in control.farm.commands(h))]
+    assert joins == ["m2", "m3"]
+
+
+def test_install_failure_then_resume(control):
+    _cluster()
+    control.farm.add_rule(r"^kubeadm join", rc=1, stderr="connection refused", times=1)
+    e = deploy.create("demo", "install", run="inline")
+    assert e["state"] == "FAILURE"
+    st = {s["name"]: s["status"] for s in e["steps"]}
+    assert st["master"] == "success" and st["worker"] == "error" and st["addon"] == "pending"
+    assert clusters.get_cluster("demo").status == "ERROR"
+    n_init = sum(c.startswith("kubeadm init --config") for c in control.farm.commands("m1"))
+    e = deploy.create("demo", "install", {"resume": True}, run="inline")
+    assert e["state"] == "SUCCESS", e["result_summary"].get("dark")
+    # resumed run skipped the finished steps: kubeadm init did not run again
+    assert sum(c.startswith("kubeadm init --config") for c in control.farm.commands("m1")) == n_init
+
+
+def test_unreachable_host_fails_install(control):
+    _cluster()
+    control.farm.unreachable.add("w1")
+    e = deploy.create("demo", "install", run="inline")
+    assert e["state"] == "FAILURE"
+    assert "w1" in e["result_summary"]["dark"]
+
+
+def test_busy_cluster_rejects_second_operation(control):
+    _cluster()
+    deploy.create("demo", "install", run="none")
+    with pytest.raises(clusters.Conflict):
+        deploy.create("demo", "gpu-validate", run="none")
+
+
+def test_unknown_operation(control):
+    _cluster()
+    with pytest.raises(ValueError):
+        deploy.create("demo", "explode", run="none")

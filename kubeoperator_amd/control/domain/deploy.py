@@ -50,6 +50,10 @@ def create(cluster_name: str, operation: str, params: dict | None = None, user: 
     with session_scope() as s:
         busy = s.scalar(select(M.Execution).where(M.Execution.project_id == c.project_id, M.Execution.kind == "deploy",
                                                   M.Execution.state.in_(("PENDING", "STARTED"))))
+        if busy is not None and _stale(s, busy):
+            busy.state, busy.date_end = "FAILURE", M.now()
+            busy.result_summary = {"error": "abandoned: no job was ever run for this execution"}
+            busy = None
         if busy is not None:
             raise clusters.Conflict(f"cluster {cluster_name} is busy with {busy.operation} ({busy.id})")
         if c.deploy_type == "AUTOMATIC" and operation in ("install", "scale"):
@@ -70,6 +74,13 @@ def create(cluster_name: str, operation: str, params: dict | None = None, user: 
     return get(eid)
 
 
+def _stale(s, e: M.Execution) -> bool:
+    """A PENDING/STARTED execution whose job is missing or finished (e.g. a client died between creating the
+    execution and queueing it) must not lock the cluster forever."""
+    j = s.get(M.Job, e.id)
+    return j is None or j.state in ("SUCCESS", "FAILURE")
+
+
 def get(execution_id: str) -> dict:
     with session_scope() as s:
         e = s.get(M.Execution, execution_id)
@@ -84,7 +95,8 @@ def get(execution_id: str) -> dict:
 def to_json(execution_id: str) -> dict:
     """What the progress websocket pushes (reference DeployExecution.to_json)."""
     d = get(execution_id)
-    return {"steps": d["steps"], "operation": d["operation"], "state": d["state"], "current_step": d["current_step"],
+    return {"id": d["id"], "steps": d["steps"], "operation": d["operation"], "state": d["state"],
+            "current_step": d["current_step"],
             "timedelta": d["timedelta"]}
 
 

@@ -10,6 +10,9 @@ recorded, so tests assert on the exact command stream; fault injection comes fro
 """
 from __future__ import annotations
 
+import base64
+import json
+import os
 import time
 
 from .transport import CmdResult, FakeTransport
@@ -33,10 +36,17 @@ users:
 
 
 class SimFarm(FakeTransport):
-    def __init__(self, gpu_hosts: set | None = None, gpus_per_host: int = 8, latency_s: float = 0.0):
+    def __init__(self, gpu_hosts: set | None = None, gpus_per_host: int = 8, latency_s: float = 0.0,
+                 state_path: str | None = None):
         super().__init__(latency_s=latency_s)
+        self.state_path = state_path  # persist host file systems across processes (kubeopsctl sim mode)
+        if state_path and os.path.exists(state_path):
+            with open(state_path) as f:
+                st = json.load(f)
+            self.fs = {h: {p: base64.b64decode(v) for p, v in files.items()} for h, files in st["fs"].items()}
+            self._addr = dict(st.get("addr", {}))
         self.gpu_hosts = set(gpu_hosts or ())  # inventory names or addresses of the GPU machines
-        self._addr: dict[str, str] = {}
+        self._addr: dict[str, str] = getattr(self, "_addr", {})
         self.gpus_per_host = gpus_per_host
         self._install_rules()
 
@@ -55,12 +65,32 @@ class SimFarm(FakeTransport):
         return fs
 
     def is_gpu(self, host: str) -> bool:
-        return host in self.gpu_hosts or self._addr.get(host) in self.gpu_hosts
+        return "*" in self.gpu_hosts or host in self.gpu_hosts or self._addr.get(host) in self.gpu_hosts
 
     def run(self, conn, cmd, timeout=3600, env=None, stdin=None):
         self._addr[conn.name] = conn.address
         self._seed(conn.name)
-        return super().run(conn, cmd, timeout, env, stdin)
+        try:
+            return super().run(conn, cmd, timeout, env, stdin)
+        finally:
+            self._save()
+
+    def put(self, conn, data, dest, mode=None):
+        try:
+            return super().put(conn, data, dest, mode)
+        finally:
+            self._save()
+
+    def _save(self):
+        if not self.state_path:
+            return
+        with self._lock:
+            st = {"fs": {h: {p: base64.b64encode(v).decode() for p, v in files.items()} for h, files in self.fs.items()},
+                  "addr": self._addr}
+            tmp = self.state_path + ".tmp"
+            with open(tmp, "w") as f:
+                json.dump(st, f)
+            os.replace(tmp, self.state_path)
 
     def get(self, conn, src):
         self._seed(conn.name)

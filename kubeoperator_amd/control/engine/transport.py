@@ -298,6 +298,9 @@ class FakeTransport(Transport):
         return d[src]
 
 
+_SIM = None
+
+
 def make_transport(kind: str, **kw) -> Transport:
     if kind == "ssh":
         return SSHTransport(**kw)
@@ -305,4 +308,15 @@ def make_transport(kind: str, **kw) -> Transport:
         return LocalTransport(**kw)
     if kind == "fake":
         return FakeTransport(**kw)
+    if kind == "sim":  # one simulated farm per process, so host state persists across operations
+        global _SIM
+        if _SIM is None:
+            from .simfarm import SimFarm
+
+            gpu = [h for h in os.environ.get("KOP_SIM_GPU_HOSTS", "*").split(",") if h]
+            from ..conf import get_config
+
+            _SIM = SimFarm(gpu_hosts=set(gpu), latency_s=float(os.environ.get("KOP_SIM_LATENCY_S", "0")),
+                           state_path=os.path.join(get_config().data_dir, "simfarm.json"))
+        return _SIM
     raise ValueError(f"unknown transport {kind!r}")

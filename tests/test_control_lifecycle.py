@@ -130,9 +130,13 @@ def test_unreachable_host_fails_install(control):
 
 def test_busy_cluster_rejects_second_operation(control):
     _cluster()
-    deploy.create("demo", "install", run="none")
+    deploy.create("demo", "install", run="queue")  # no worker running: stays PENDING
     with pytest.raises(clusters.Conflict):
         deploy.create("demo", "gpu-validate", run="none")
+    # an execution that never got a job (client died) does not lock the cluster
+    clusters.create_cluster({"name": "demo2", "template": "single-master"})
+    deploy.create("demo2", "install", run="none")
+    deploy.create("demo2", "gpu-validate", run="none")
 
 
 def test_unknown_operation(control):

@@ -1,0 +1,120 @@
+"""The control plane's own ASGI server over real sockets: HTTP keep-alive + chunked responses, the
+progress websocket (RFC 6455 handshake, masked client frames, close), and the kubeopsctl service launcher
+(start -d / status / stop with pidfiles, reference core/kubeops.py)."""
+import asyncio
+import base64
+import json
+import os
+import socket
+import struct
+import subprocess
+import sys
+import threading
+import time
+
+import httpx
+import pytest
+
+from kubeoperator_amd.control.api import create_app
+from kubeoperator_amd.control.api.server import Server
+
+
+@pytest.fixture
+def live(control):
+    srv = Server(create_app(), "127.0.0.1", 0)
+    loop = asyncio.new_event_loop()
+    ready = threading.Event()
+
+    def run():
+        asyncio.set_event_loop(loop)
+        loop.run_until_complete(srv.start())
+        ready.set()
+        loop.run_forever()
+
+    t = threading.Thread(target=run, daemon=True)
+    t.start()
+    assert ready.wait(10)
+    yield f"127.0.0.1:{srv.port}"
+    asyncio.run_coroutine_threadsafe(srv.stop(), loop).result(10)
+    loop.call_soon_threadsafe(loop.stop)
+    t.join(5)
+
+
+def _ws_connect(addr, path):
+    host, port = addr.split(":")
+    s = socket.create_connection((host, int(port)), timeout=10)
+    key = base64.b64encode(os.urandom(16)).decode()
+    s.sendall((f"GET {path} HTTP/1.1\r\nHost: {addr}\r\nUpgrade: websocket\r\nConnection: Upgrade\r\n"
+               f"Sec-WebSocket-Key: {key}\r\nSec-WebSocket-Version: 13\r\n\r\n").encode())
+    head = b""
+    while b"\r\n\r\n" not in head:
+        head += s.recv(1)
+    assert head.startswith(b"HTTP/1.1 101"), head
+    return s
+
+
+def _ws_recv(s):
+    b1, b2 = s.recv(2, socket.MSG_WAITALL)
+    n = b2 & 0x7F
+    if n == 126:
+        n = struct.unpack("!H", s.recv(2, socket.MSG_WAITALL))[0]
+    elif n == 127:
+        n = struct.unpack("!Q", s.recv(8, socket.MSG_WAITALL))[0]
+    data = s.recv(n, socket.MSG_WAITALL) if n else b""
+    return b1 & 0x0F, data
+
+
+def _ws_send_close(s):
+    mask = os.urandom(4)
+    payload = struct.pack("!H", 1000)
+    s.sendall(bytes([0x88, 0x80 | len(payload)]) + mask + bytes(b ^ mask[i & 3] for i, b in enumerate(payload)))
+
+
+def test_http_keepalive_and_auth(live):
+    with httpx.Client(base_url=f"http://{live}") as c:
+        assert c.get("/healthz").json()["ok"]
+        tok = c.post("/api/v1/token/auth/", json={"username": "admin", "password": "kubeoperator@admin123"}).json()["token"]
+        c.headers["Authorization"] = f"JWT {tok}"
+        for _ in range(3):  # same connection
+            assert c.get("/api/v1/packages/").status_code == 200
+        assert c.get("/api/v1/clusters/nope/").status_code == 404
+        r = c.get("/ui/")
+        assert r.status_code == 200 and "<html" in r.text.lower()
+
+
+def test_progress_websocket(live, control):
+    from kubeoperator_amd.control.domain import clusters, deploy, hosts
+    hosts.create_host({"name": "m1", "ip": "10.0.0.1", "password": "pw"})
+    clusters.create_cluster({"name": "demo", "template": "single-master"})
+    clusters.add_node("demo", {"name": "m1", "host": "m1", "roles": ["master"]})
+    e = deploy.create("demo", "uninstall", run="inline")
+    s = _ws_connect(live, f"/ws/progress/{e['id']}/")
+    op, data = _ws_recv(s)
+    assert op == 1
+    msg = json.loads(data)
+    assert msg["id"] == e["id"] and msg["state"] == e["state"]
+    op, _ = _ws_recv(s)  # server closes after a finished execution
+    assert op == 8
+    _ws_send_close(s)
+    s.close()
+
+
+def test_service_launcher(tmp_path):
+    cfgp = tmp_path / "config.yml"
+    cfgp.write_text(f"DATA_DIR: {tmp_path}/data\nHTTP_LISTEN_PORT: 0\nHTTP_BIND_HOST: 127.0.0.1\n")
+    env = dict(os.environ, KUBEOPERATOR_CONFIG=str(cfgp), KOP_PBKDF2_ITERS="1000")
+    run = lambda *a: subprocess.run([sys.executable, "-m", "kubeoperator_amd.control.cli", *a], env=env,  # noqa: E731
+                                    capture_output=True, text=True, timeout=60)
+    r = run("start", "worker", "-d")
+    assert r.returncode == 0, r.stdout + r.stderr
+    try:
+        r = run("status", "worker")
+        assert "running" in r.stdout
+    finally:
+        r = run("stop", "worker")
+    assert "stopped" in r.stdout
+    for _ in range(50):
+        if "stopped" in run("status", "worker").stdout:
+            break
+        time.sleep(0.1)
+    assert "stopped" in run("status", "worker").stdout

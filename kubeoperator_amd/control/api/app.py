@@ -1007,9 +1007,20 @@ def create_app() -> FastAPI:
     app.include_router(r)
 
     # ------------------------------------------------------------------ websockets (ws.py consumers)
+    async def _ws_auth(ws: WebSocket) -> bool:
+        tok = ws.query_params.get("token") or _auth_token(ws.headers)
+        try:
+            await asyncio.to_thread(users.user_from_token, tok or "")
+            return True
+        except AuthError:
+            await ws.close(code=4401)
+            return False
+
     @app.websocket("/ws/progress/{eid}/")
     async def ws_progress(ws: WebSocket, eid: str):
         """Push DeployExecution.to_json() every second (reference kubeops_api/ws.py:8-31)."""
+        if not await _ws_auth(ws):
+            return
         await ws.accept()
         try:
             while True:
@@ -1025,6 +1036,8 @@ def create_app() -> FastAPI:
     @app.websocket("/ws/tasks/{jid}/log/")
     async def ws_task_log(ws: WebSocket, jid: str):
         """Tail the job log: up to 4 KiB every 0.2 s (reference celery_api/ws.py:8-42)."""
+        if not await _ws_auth(ws):
+            return
         await ws.accept()
         off = 0
         path = jobs.log_path(jid)

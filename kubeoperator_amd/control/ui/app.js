@@ -1,0 +1,468 @@
+// KubeOperator-AMD web UI: a dependency-free single-page app over /api/v1 and the two websockets.
+// Module map follows the reference UI (SURVEY.md §2.9): sign-in, dashboard, clusters (list, create wizard
+// with device checks, detail tabs: overview / nodes / deploy progress + live log / health / events / backup /
+// grade / configs), hosts (+import), credentials, regions / zones / plans, packages, NFS / Ceph, items + members
+// + resources, users, settings (system, backup storage, LDAP, notification), message center, system log.
+"use strict";
+
+const API = "/api/v1";
+const $ = (sel, el = document) => el.querySelector(sel);
+const esc = (s) => String(s ?? "").replace(/[&<>"']/g, (c) => ({"&": "&amp;", "<": "&lt;", ">": "&gt;", '"': "&quot;", "'": "&#39;"}[c]));
+const st = (s) => `<span class="status ${esc(s)}">${esc(s)}</span>`;
+let ME = null;
+
+// ------------------------------------------------------------------ API client (JWT header, refresh)
+async function api(method, path, body, opts = {}) {
+  const headers = {};
+  const tok = localStorage.getItem("kop_token");
+  if (tok) headers.Authorization = "JWT " + tok;
+  let payload;
+  if (body instanceof FormData) payload = body;
+  else if (body !== undefined) { headers["Content-Type"] = "application/json"; payload = JSON.stringify(body); }
+  const r = await fetch(API + path, {method, headers, body: payload});
+  if (r.status === 401 && !opts.noAuthRedirect) { logout(); throw new Error("session expired"); }
+  if (opts.raw) return r;
+  const text = await r.text();
+  const data = text ? (() => { try { return JSON.parse(text); } catch { return text; } })() : null;
+  if (!r.ok) throw new Error((data && (data.detail || JSON.stringify(data))) || r.statusText);
+  return data;
+}
+const GET = (p) => api("GET", p), POST = (p, b) => api("POST", p, b ?? {}), PUT = (p, b) => api("PUT", p, b ?? {}),
+  PATCH = (p, b) => api("PATCH", p, b ?? {}), DEL = (p) => api("DELETE", p);
+
+function wsURL(path) { return (location.protocol === "https:" ? "wss://" : "ws://") + location.host + path; }
+
+async function refreshToken() {
+  const tok = localStorage.getItem("kop_token");
+  if (!tok) return;
+  try { const r = await api("POST", "/token/refresh/", {token: tok}, {noAuthRedirect: true}); localStorage.setItem("kop_token", r.token); }
+  catch { /* expired: next call redirects */ }
+}
+
+// ------------------------------------------------------------------ auth
+function logout() { localStorage.removeItem("kop_token"); ME = null; showLogin(); }
+function showLogin() { $("#shell").classList.add("hidden"); $("#login").classList.remove("hidden"); }
+$("#login-form").addEventListener("submit", async (e) => {
+  e.preventDefault();
+  const f = new FormData(e.target);
+  try {
+    const r = await api("POST", "/token/auth/", {username: f.get("username"), password: f.get("password")}, {noAuthRedirect: true});
+    localStorage.setItem("kop_token", r.token);
+    $("#login-error").textContent = "";
+    boot();
+  } catch (err) { $("#login-error").textContent = err.message; }
+});
+$("#logout").onclick = logout;
+
+// ------------------------------------------------------------------ helpers: tables, forms, modal
+function table(rows, cols, empty = "Nothing here yet.") {
+  if (!rows || !rows.length) return `<p class="muted">${empty}</p>`;
+  return `<table><tr>${cols.map((c) => `<th>${esc(c[0])}</th>`).join("")}</tr>${rows.map((r) =>
+    `<tr>${cols.map((c) => `<td>${typeof c[1] === "function" ? c[1](r) : esc(r[c[1]])}</td>`).join("")}</tr>`).join("")}</table>`;
+}
+function kv(obj) {
+  return `<table class="kv">${Object.entries(obj).map(([k, v]) => `<tr><td>${esc(k)}</td><td>${typeof v === "object" ? `<code>${esc(JSON.stringify(v))}</code>` : esc(v)}</td></tr>`).join("")}</table>`;
+}
+function modal(html) { $("#modal-body").innerHTML = html; $("#modal").classList.remove("hidden"); }
+function closeModal() { $("#modal").classList.add("hidden"); }
+$("#modal").addEventListener("click", (e) => { if (e.target.id === "modal") closeModal(); });
+
+// fields: [name, label, type("text"|"password"|"number"|"select"|"textarea"|"json"|"checkbox"), options|default]
+function formModal(title, fields, onSubmit, initial = {}) {
+  const inputs = fields.map(([name, label, type = "text", opt]) => {
+    const v = initial[name] ?? (type === "select" ? "" : (opt ?? ""));
+    if (type === "select") return `<label>${esc(label)}<select name="${name}">${(opt || []).map((o) => {
+      const [val, txt] = Array.isArray(o) ? o : [o, o];
+      return `<option value="${esc(val)}" ${String(val) === String(v) ? "selected" : ""}>${esc(txt)}</option>`; }).join("")}</select></label>`;
+    if (type === "textarea" || type === "json") return `<label>${esc(label)}<textarea name="${name}">${esc(type === "json" ? JSON.stringify(v || {}, null, 2) : v)}</textarea></label>`;
+    if (type === "checkbox") return `<label><input type="checkbox" name="${name}" style="width:auto" ${v ? "checked" : ""}> ${esc(label)}</label>`;
+    return `<label>${esc(label)}<input name="${name}" type="${type}" value="${esc(v)}"></label>`;
+  }).join("");
+  modal(`<h2>${esc(title)}</h2><form id="mf">${inputs}<div class="toolbar"><button type="submit">OK</button>
+    <button type="button" class="secondary" onclick="closeModal()">Cancel</button></div><p class="error" id="mf-err"></p></form>`);
+  $("#mf").addEventListener("submit", async (e) => {
+    e.preventDefault();
+    const out = {};
+    for (const [name, , type] of fields) {
+      const el = e.target.elements[name];
+      if (type === "number") out[name] = el.value === "" ? null : Number(el.value);
+      else if (type === "json") { try { out[name] = JSON.parse(el.value || "{}"); } catch (err) { $("#mf-err").textContent = `${name}: ${err.message}`; return; } }
+      else if (type === "checkbox") out[name] = el.checked;
+      else out[name] = el.value;
+    }
+    try { await onSubmit(out); closeModal(); route(); } catch (err) { $("#mf-err").textContent = err.message; }
+  });
+}
+async function confirmDo(text, fn) { if (confirm(text)) { try { await fn(); route(); } catch (e) { alert(e.message); } } }
+
+// generic CRUD page for simple resources
+function crudPage(title, path, cols, fields, opts = {}) {
+  return async (v) => {
+    const rows = await GET(path);
+    const list = Array.isArray(rows) ? rows : rows.results;
+    v.innerHTML = `<h2>${esc(title)}</h2><div class="toolbar">${opts.readonly ? "" : `<button id="add">Add</button>`}${opts.extraButtons || ""}</div>
+      ${table(list, [...cols, ...(opts.readonly ? [] : [["", (r) => `<button class="link" data-edit="${esc(r.id)}">edit</button><button class="link" data-del="${esc(r.id)}">delete</button>`]])])}`;
+    if (opts.readonly) return;
+    $("#add").onclick = () => formModal(`Add ${title}`, fields, (d) => POST(path, opts.prepare ? opts.prepare(d) : d));
+    v.querySelectorAll("[data-edit]").forEach((b) => b.onclick = () => {
+      const row = list.find((r) => r.id === b.dataset.edit);
+      formModal(`Edit ${title}`, fields, (d) => PATCH(`${path}${row.id}/`, opts.prepare ? opts.prepare(d) : d), row);
+    });
+    v.querySelectorAll("[data-del]").forEach((b) => b.onclick = () => confirmDo("Delete?", () => DEL(`${path}${b.dataset.del}/`)));
+    if (opts.after) opts.after(v, list);
+  };
+}
+
+// ------------------------------------------------------------------ views
+const views = {};
+
+views.dashboard = async (v) => {
+  const [clusters, hosts, dash] = await Promise.all([GET("/clusters/"), GET("/host/"), GET("/dashboard/all/all/").catch(() => ({}))]);
+  const gpus = hosts.reduce((a, h) => a + (h.gpu_num || 0), 0);
+  const running = clusters.filter((c) => c.status === "RUNNING").length;
+  v.innerHTML = `<h2>Dashboard</h2><div class="grid">
+    <div class="card stat"><div class="v">${clusters.length}</div><div class="k">clusters (${running} running)</div></div>
+    <div class="card stat"><div class="v">${hosts.length}</div><div class="k">hosts</div></div>
+    <div class="card stat"><div class="v">${gpus}</div><div class="k">AMD Instinct GPUs registered</div></div>
+    <div class="card stat"><div class="v">${dash.gpu_allocatable ?? 0}/${dash.gpu_total ?? 0}</div><div class="k">amd.com/gpu allocatable / capacity</div></div>
+    </div><h3>Clusters</h3>${table(clusters, [["Name", (c) => `<a href="#/cluster/${esc(c.name)}">${esc(c.name)}</a>`], ["Status", (c) => st(c.status)],
+      ["Template", "template"], ["Nodes", "node_size"], ["GPUs", "gpu_num"], ["Package", "package"]])}
+    <h3>Pods restarting / failing</h3>${table([...(dash.restart_pods || []), ...(dash.error_pods || [])], [["Namespace", "namespace"], ["Pod", "name"], ["Status", "status"], ["Restarts", "restart_count"]], "All pods healthy (or no monitoring data yet).")}`;
+};
+
+views.clusters = async (v) => {
+  const rows = await GET("/clusters/");
+  v.innerHTML = `<h2>Clusters</h2><div class="toolbar"><button id="new">Create cluster</button></div>
+    ${table(rows, [["Name", (c) => `<a href="#/cluster/${esc(c.name)}">${esc(c.name)}</a>`], ["Status", (c) => st(c.status)], ["Template", "template"],
+      ["Deploy", "deploy_type"], ["Nodes", "node_size"], ["GPUs", "gpu_num"], ["Package", "package"], ["Item", "item_name"],
+      ["", (c) => `<button class="link" data-del="${esc(c.name)}">delete</button>`]])}`;
+  $("#new").onclick = () => { location.hash = "#/cluster-create"; };
+  v.querySelectorAll("[data-del]").forEach((b) => b.onclick = () => confirmDo(`Delete cluster ${b.dataset.del}?`, () => DEL(`/clusters/${b.dataset.del}/`)));
+};
+
+// create wizard: template -> package -> network -> storage -> nodes -> device checks (cluster-create.component.ts)
+views["cluster-create"] = async (v) => {
+  const [plan, pkgs, hosts, items, plans] = await Promise.all([GET("/cluster/config"), GET("/packages/"), GET("/host/"), GET("/items/"), GET("/plans/")]);
+  const free = hosts.filter((h) => !h.node_id);
+  const tmpls = plan.templates || [];
+  v.innerHTML = `<h2>Create cluster</h2><form id="cc" class="card">
+    <div class="row"><label>Name<input name="name" required pattern="[a-zA-Z0-9-]+"></label>
+      <label>Item<select name="item_name">${items.map((i) => `<option>${esc(i.name)}</option>`).join("")}</select></label></div>
+    <div class="row"><label>Template<select name="template">${tmpls.map((t) => `<option value="${esc(t.name)}">${esc(t.name)}${t.comment ? " — " + esc(t.comment) : ""}</option>`).join("")}</select></label>
+      <label>Package<select name="package">${pkgs.map((p) => `<option value="${esc(p.name)}">${esc(p.name)} (${esc(p.meta.version || "")})</option>`).join("")}</select></label></div>
+    <div class="row"><label>Deploy type<select name="deploy_type"><option>MANUAL</option><option>AUTOMATIC</option></select></label>
+      <label>IaaS plan (AUTOMATIC)<select name="plan"><option value="">—</option>${plans.map((p) => `<option value="${esc(p.id)}">${esc(p.name)}</option>`).join("")}</select></label>
+      <label>Workers (AUTOMATIC)<input name="worker_size" type="number" value="1"></label></div>
+    <div class="row"><label>Network<select name="network_plugin">${(plan.networks || []).map((n) => `<option>${esc(n.name)}</option>`).join("")}</select></label>
+      <label>Storage<select name="persistent_storage">${(plan.storages || []).map((s) => `<option>${esc(s.name)}</option>`).join("")}</select></label>
+      <label>Domain suffix<input name="cluster_doamin_suffix" value="cluster.local"></label></div>
+    <label><input type="checkbox" name="gpu_install" style="width:auto" checked> Install ROCm + AMD device plugin on GPU nodes</label>
+    <h3>Nodes (MANUAL)</h3><div id="nodes"></div>
+    <div id="checks"></div>
+    <div class="toolbar"><button type="submit">Create</button><button type="button" id="cc-install" class="secondary">Create &amp; install</button></div>
+    <p class="error" id="cc-err"></p></form>`;
+  const form = $("#cc");
+  const renderNodes = () => {
+    const t = tmpls.find((x) => x.name === form.template.value) || {roles: []};
+    const roles = (t.roles || []).map((r) => r.name);
+    $("#nodes").innerHTML = table(free, [["Host", "name"], ["IP", "ip"], ["CPU", "cpu_core"], ["Mem MiB", "memory"], ["GPUs", (h) => `${h.gpu_num || 0} ${esc(h.gpu_info || "")}`],
+      ["Role", (h) => `<select data-host="${esc(h.name)}"><option value="">(not used)</option>${roles.map((r) => `<option>${esc(r)}</option>`).join("")}</select>`]], "No free hosts: register hosts first.");
+    $("#nodes").querySelectorAll("select").forEach((s) => s.onchange = checkDevices);
+  };
+  // device checks against template meta.requires (device-check.service.ts)
+  const checkDevices = () => {
+    const t = tmpls.find((x) => x.name === form.template.value) || {};
+    const msgs = [];
+    const counts = {};
+    $("#nodes").querySelectorAll("select").forEach((s) => {
+      if (!s.value) return;
+      counts[s.value] = (counts[s.value] || 0) + 1;
+      const h = free.find((x) => x.name === s.dataset.host);
+      const req = ((t.roles || []).find((r) => r.name === s.value) || {}).meta?.requires || {};
+      for (const d of req.device_require || []) {
+        const have = d.name === "memory_size" ? (h.memory || 0) / 1024 : (h[d.name] || 0);
+        if (have < d.minimal) msgs.push(`${h.name}: ${d.verbose} ${have.toFixed ? have.toFixed(0) : have} < ${d.minimal} ${d.unit || ""}`);
+      }
+    });
+    for (const r of t.roles || []) {
+      const need = r.meta?.requires?.nodes_require;
+      if (!Array.isArray(need) || r.meta?.hidden) continue;
+      const n = counts[r.name] || 0, [op, k] = need;
+      const ok = op === "=" ? n === k : op === ">=" ? n >= k : op === ">" ? n > k : true;
+      if (!ok) msgs.push(`role ${r.name}: needs ${op} ${k} node(s), selected ${n}`);
+    }
+    $("#checks").innerHTML = msgs.length ? `<p class="error">${msgs.map(esc).join("<br>")}</p>` : "";
+  };
+  form.template.onchange = renderNodes;
+  renderNodes();
+  const submit = async (install) => {
+    const f = new FormData(form);
+    const d = Object.fromEntries(f.entries());
+    d.configs = {gpu_install: !!form.gpu_install.checked};
+    delete d.gpu_install;
+    d.worker_size = Number(d.worker_size || 1);
+    if (!d.plan) delete d.plan;
+    d.nodes = [];
+    $("#nodes").querySelectorAll("select").forEach((s) => { if (s.value) d.nodes.push({name: s.dataset.host, host: s.dataset.host, roles: [s.value]}); });
+    try {
+      const c = await POST("/clusters/", d);
+      if (install) await POST(`/clusters/${c.name}/executions/`, {operation: "install", params: {}});
+      location.hash = `#/cluster/${c.name}/${install ? "deploy" : "overview"}`;
+    } catch (e) { $("#cc-err").textContent = e.message; }
+  };
+  form.addEventListener("submit", (e) => { e.preventDefault(); submit(false); });
+  $("#cc-install").onclick = () => submit(true);
+};
+
+const OPS = [["install", "Install"], ["gpu-validate", "Validate GPUs"], ["upgrade", "Upgrade"], ["scale", "Scale (IaaS)"],
+  ["add-worker", "Add worker"], ["remove-worker", "Remove worker"], ["backup", "Backup"], ["restore", "Restore"],
+  ["bigip-config", "F5 BIG-IP"], ["uninstall", "Uninstall"]];
+
+async function runOp(c, op) {
+  const params = {};
+  const go = async (p) => { const e = await POST(`/clusters/${c.name}/executions/`, {operation: op, params: p}); location.hash = `#/cluster/${c.name}/deploy/${e.id}`; };
+  if (op === "upgrade") {
+    const pk = await GET("/packages/");
+    return formModal("Upgrade", [["package", "Package", "select", pk.map((p) => p.name)]], (d) => go(d));
+  }
+  if (op === "scale") return formModal("Scale workers", [["num", "Worker count", "number", c.worker_size]], (d) => go(d));
+  if (op === "add-worker") {
+    const hosts = (await GET("/host/")).filter((h) => !h.node_id);
+    return formModal("Add worker", [["host", "Host", "select", hosts.map((h) => h.name)]], (d) => go(d));
+  }
+  if (op === "remove-worker") {
+    const nodes = (await GET(`/clusters/${c.name}/nodes/`)).filter((n) => (n.roles || []).includes("worker") || (n.groups || []).includes("worker"));
+    return formModal("Remove worker", [["node", "Node", "select", nodes.map((n) => n.name)]], (d) => go(d));
+  }
+  if (op === "backup") {
+    const s = await GET("/backupStorage/");
+    return formModal("Backup", [["backupStorageId", "Storage", "select", s.map((x) => [x.id, x.name])]], (d) => go(d));
+  }
+  if (op === "restore") {
+    const b = await GET(`/clusterBackup/${c.project_id}/`);
+    return formModal("Restore", [["clusterBackupId", "Backup", "select", b.map((x) => [x.id, x.name])]], (d) => go(d));
+  }
+  if (!confirm(`${op} cluster ${c.name}?`)) return;
+  await go(params);
+}
+
+let liveSockets = [];
+function closeSockets() { liveSockets.forEach((s) => { try { s.close(); } catch { /* ignore */ } }); liveSockets = []; }
+
+views.cluster = async (v, [name, tab = "overview", arg]) => {
+  const c = await GET(`/clusters/${name}/`);
+  const tabs = ["overview", "nodes", "deploy", "health", "events", "backup", "grade", "configs", "apps"];
+  v.innerHTML = `<h2>${esc(c.name)} ${st(c.status)}</h2><div class="tabs">${tabs.map((t) => `<a href="#/cluster/${esc(name)}/${t}" class="${t === tab ? "active" : ""}">${t}</a>`).join("")}</div><div id="tab"></div>`;
+  const t = $("#tab");
+  if (tab === "overview") {
+    t.innerHTML = `<div class="toolbar">${OPS.map(([op, label]) => `<button class="${op === "uninstall" ? "" : "secondary"}" data-op="${op}">${label}</button>`).join("")}
+      <a href="${API}/cluster/${esc(c.name)}/download/" id="kc">kubeconfig</a></div>${kv({template: c.template, package: c.package, network: c.network_plugin,
+      storage: c.persistent_storage, deploy_type: c.deploy_type, nodes: c.node_size, gpus: c.gpu_num, domain: c.cluster_doamin_suffix, item: c.item_name,
+      created: c.date_created, last_operation: c.current_execution ? `${c.current_execution.operation} ${c.current_execution.state}` : "—"})}`;
+    t.querySelectorAll("[data-op]").forEach((b) => b.onclick = () => runOp(c, b.dataset.op).catch((e) => alert(e.message)));
+    $("#kc").onclick = async (e) => { e.preventDefault(); const r = await api("GET", `/cluster/${c.name}/download/`, undefined, {raw: true}); const blob = await r.blob();
+      const a = document.createElement("a"); a.href = URL.createObjectURL(blob); a.download = `${c.name}-kubeconfig`; a.click(); };
+  } else if (tab === "nodes") {
+    const nodes = await GET(`/clusters/${name}/nodes/`);
+    t.innerHTML = table(nodes, [["Name", "name"], ["IP", "ip"], ["Roles", (n) => esc((n.roles || n.groups || []).join(", "))], ["GPUs", (n) => esc((n.vars || {}).gpu_num || 0)],
+      ["Conditions", (n) => (n.conditions || []).map((x) => st(`${x.type}:${x.status}`)).join(" ")]]);
+  } else if (tab === "deploy") {
+    const execs = await GET(`/clusters/${name}/executions/`);
+    const cur = arg || (execs[0] && execs[0].id);
+    t.innerHTML = `<div class="row"><div style="flex:0 0 320px">${table(execs, [["Operation", (e) => `<a href="#/cluster/${esc(name)}/deploy/${esc(e.id)}">${esc(e.operation)}</a>`],
+      ["State", (e) => st(e.state)], ["Time", (e) => `${(e.timedelta || 0).toFixed(1)}s`]])}</div>
+      <div><div id="steps" class="steps"></div><pre class="term" id="term"></pre></div></div>`;
+    if (cur) follow(cur);
+  } else if (tab === "health") {
+    const [h, hist] = await Promise.all([GET(`/cluster/${name}/health/all/`).catch((e) => ({error: e.message})), GET(`/clusterHealthHistory/${c.project_id}/`).catch(() => [])]);
+    t.innerHTML = h.error ? `<p class="muted">${esc(h.error)}</p>` : kv(h) + `<h3>Availability history</h3>` + table(hist, [["Date", "date_created"], ["Rate", "available_rate"], ["Type", "date_type"]]);
+  } else if (tab === "events") {
+    const ev = await POST(`/cluster/${name}/event/`, {limit: 200}).catch((e) => ({items: [], error: e.message}));
+    t.innerHTML = table(ev.items || ev, [["Time", "last_timestamp"], ["Type", (e) => st(e.type)], ["Reason", "reason"], ["Object", "name"], ["Message", "message"]], ev.error || "No events.");
+  } else if (tab === "backup") {
+    const [bks, strat, stores] = await Promise.all([GET(`/clusterBackup/${c.project_id}/`), GET("/backupStrategy/"), GET("/backupStorage/")]);
+    const mine = strat.find((s) => s.cluster_id === c.id);
+    t.innerHTML = `<h3>Strategy</h3>${mine ? kv(mine) : "<p class='muted'>none</p>"}<div class="toolbar"><button id="strat" class="secondary">Set strategy</button></div>
+      <h3>Backups</h3>${table(bks, [["Name", "name"], ["Size", "size"], ["Date", "date_created"], ["", (b) => `<button class="link" data-restore="${esc(b.id)}">restore</button><button class="link" data-del="${esc(b.id)}">delete</button>`]])}`;
+    $("#strat").onclick = () => formModal("Backup strategy", [["backup_storage_id", "Storage", "select", stores.map((s) => [s.id, s.name])], ["cron", "Every N days", "number", 1],
+      ["save_num", "Keep", "number", 7], ["status", "Status", "select", ["ENABLE", "DISABLE"]]],
+      (d) => mine ? PATCH(`/backupStrategy/${mine.id}/`, d) : POST("/backupStrategy/", {...d, cluster_id: c.id}), mine || {});
+    t.querySelectorAll("[data-restore]").forEach((b) => b.onclick = () => confirmDo("Restore this backup?", () => POST("/clusterBackup/restore/", {id: b.dataset.restore})));
+    t.querySelectorAll("[data-del]").forEach((b) => b.onclick = () => confirmDo("Delete backup?", () => DEL(`/clusterBackup/${b.dataset.del}/delete/`)));
+  } else if (tab === "grade") {
+    const g = await GET(`/cluster/${name}/grade/`).catch((e) => ({error: e.message}));
+    t.innerHTML = g.error ? `<p class="muted">${esc(g.error)}</p>` : `<div class="grid"><div class="card stat"><div class="v">${g.score}</div><div class="k">score</div></div></div>` +
+      table(g.results, [["Namespace", "namespace"], ["Workload", "name"], ["Container", "container"], ["Findings", (r) => r.results.filter((x) => !x.success).map((x) => st(x.id)).join(" ")]]);
+  } else if (tab === "configs") {
+    const cfgs = await GET(`/clusters/${name}/configs/`);
+    t.innerHTML = `<div class="toolbar"><button id="addcfg">Set</button></div>` + table(cfgs, [["Key", "key"], ["Value", (x) => esc(JSON.stringify(x.value))], ["", (x) => `<button class="link" data-del="${esc(x.key)}">delete</button>`]]);
+    $("#addcfg").onclick = () => formModal("Set config", [["key", "Key"], ["value", "Value (JSON)", "text"]], (d) => {
+      let val = d.value; try { val = JSON.parse(d.value); } catch { /* keep string */ }
+      return POST(`/clusters/${name}/configs/`, {key: d.key, value: val}); });
+    t.querySelectorAll("[data-del]").forEach((b) => b.onclick = () => confirmDo("Delete config?", () => DEL(`/clusters/${name}/configs/${b.dataset.del}/`)));
+  } else if (tab === "apps") {
+    t.innerHTML = table(c.apps || [], [["App", "name"], ["URL", (a) => `<a href="${esc(a.url)}" target="_blank">${esc(a.url)}</a>`], ["Description", "describe"]]);
+  }
+};
+
+function follow(eid) {
+  closeSockets();
+  const term = $("#term"), steps = $("#steps");
+  const tok = localStorage.getItem("kop_token");
+  const p = new WebSocket(wsURL(`/ws/progress/${eid}/?token=${encodeURIComponent(tok)}`));
+  p.onmessage = (m) => { const d = JSON.parse(m.data); steps.innerHTML = (d.steps || []).map((s) => `<span class="${esc(s.status)}">${esc(s.name)}</span>`).join("") + ` ${st(d.state)}`; };
+  const l = new WebSocket(wsURL(`/ws/tasks/${eid}/log/?token=${encodeURIComponent(tok)}`));
+  l.onmessage = (m) => { term.textContent += JSON.parse(m.data).message.replace(/\r\n/g, "\n"); term.scrollTop = term.scrollHeight; };
+  liveSockets.push(p, l);
+}
+
+views.hosts = async (v) => {
+  const [rows, creds, zones] = await Promise.all([GET("/host/"), GET("/credential/"), GET("/zones/")]);
+  v.innerHTML = `<h2>Hosts</h2><div class="toolbar"><button id="add">Register host</button><label class="secondary" style="margin:0">Import (.xlsx/.csv)
+    <input type="file" id="imp" accept=".xlsx,.csv" style="width:auto"></label></div>
+    ${table(rows, [["Name", "name"], ["IP", "ip"], ["Status", (h) => st(h.status)], ["OS", (h) => `${esc(h.os)} ${esc(h.os_version)}`], ["CPU", "cpu_core"], ["Mem MiB", "memory"],
+      ["GPUs", (h) => h.gpu_num ? `${h.gpu_num} × ${esc(h.gpu_info)}` : "—"], ["Cluster", (h) => h.node_id ? "in use" : ""],
+      ["", (h) => `<button class="link" data-sync="${esc(h.id)}">sync</button><button class="link" data-del="${esc(h.id)}">delete</button>`]])}`;
+  $("#add").onclick = () => formModal("Register host", [["name", "Name"], ["ip", "IP"], ["port", "SSH port", "number", 22], ["credential", "Credential", "select", [["", "(username/password below)"], ...creds.map((c) => [c.id, c.name])]],
+    ["username", "Username", "text", "root"], ["password", "Password", "password"], ["zone_id", "Zone", "select", [["", "—"], ...zones.map((z) => [z.id, z.name])]]],
+    (d) => { if (!d.credential) delete d.credential; if (!d.zone_id) delete d.zone_id; return POST("/host/", d); });
+  $("#imp").onchange = async (e) => { const fd = new FormData(); fd.append("file", e.target.files[0]); try { const r = await api("POST", "/host/import/", fd); alert(`created: ${r.created.join(", ")}\n${(r.errors || []).join("\n")}`); route(); } catch (err) { alert(err.message); } };
+  v.querySelectorAll("[data-sync]").forEach((b) => b.onclick = () => POST(`/host/${b.dataset.sync}/sync/`).then(() => setTimeout(route, 1500)));
+  v.querySelectorAll("[data-del]").forEach((b) => b.onclick = () => confirmDo("Delete host?", () => DEL(`/host/${b.dataset.del}/`)));
+};
+
+views.credentials = crudPage("Credentials", "/credential/", [["Name", "name"], ["Username", "username"], ["Type", "type"]],
+  [["name", "Name"], ["username", "Username", "text", "root"], ["type", "Type", "select", ["password", "privateKey"]], ["password", "Password", "password"], ["private_key", "Private key", "textarea"]]);
+
+views.packages = async (v) => {
+  const rows = await GET("/packages/");
+  v.innerHTML = `<h2>Offline packages</h2>${table(rows, [["Name", "name"], ["Version", (p) => esc(p.meta.version)], ["Kubernetes", (p) => esc((p.meta.vars || {}).kube_version)],
+    ["ROCm", (p) => esc((p.meta.vars || {}).rocm_version)], ["AMD device plugin", (p) => esc((p.meta.vars || {}).amd_device_plugin_image || "")], ["Path", "path"]])}`;
+};
+
+views.regions = crudPage("Regions", "/regions/", [["Name", "name"], ["Cloud region", "cloud_region"], ["Provider", (r) => esc((r.vars || {}).provider || "")]],
+  [["name", "Name"], ["cloud_region", "Cloud region"], ["template_id", "Provider template id"], ["vars", "Provider vars (JSON: provider, host/user/password …)", "json"], ["comment", "Comment"]]);
+views.zones = crudPage("Zones", "/zones/", [["Name", "name"], ["Cloud zone", "cloud_zone"], ["IP range", (z) => esc(`${(z.vars || {}).ip_start || ""} – ${(z.vars || {}).ip_end || ""}`)],
+  ["Used IPs", (z) => (z.ip_used || []).length], ["Status", (z) => st(z.status)]],
+  [["name", "Name"], ["region_id", "Region id"], ["cloud_zone", "Cloud zone"], ["vars", "Zone vars (JSON: ip_start, ip_end, net_mask, gateway, dns1 …)", "json"]]);
+views.plans = crudPage("Deploy plans", "/plans/", [["Name", "name"], ["Template", "deploy_template"], ["Zones", (p) => (p.zone_ids || []).length], ["Compute", (p) => esc(JSON.stringify(p.vars || {}))]],
+  [["name", "Name"], ["region_id", "Region id"], ["zone_ids", "Zone ids (JSON list)", "json"], ["deploy_template", "Template", "select", ["SINGLE", "MULTIPLE"]],
+   ["vars", "Vars (JSON: master_model, worker_model, gpu_worker …)", "json"]]);
+
+views.storage = async (v) => {
+  const [nfs, ceph] = await Promise.all([GET("/storage/nfs/"), GET("/storage/ceph/")]);
+  v.innerHTML = `<h2>Storage</h2><h3>NFS</h3><div class="toolbar"><button id="nfs">Add NFS</button></div>
+    ${table(nfs, [["Name", "name"], ["Server", (n) => esc((n.vars || {}).storage_nfs_server)], ["Path", (n) => esc((n.vars || {}).storage_nfs_server_path)], ["Status", (n) => st(n.status)],
+      ["", (n) => `<button class="link" data-dn="${esc(n.name)}">delete</button>`]])}
+    <h3>Ceph</h3><div class="toolbar"><button id="ceph">Add Ceph</button></div>${table(ceph, [["Name", "name"], ["Monitors", (c) => esc((c.vars || {}).monitors)],
+      ["", (c) => `<button class="link" data-dc="${esc(c.name)}">delete</button>`]])}`;
+  $("#nfs").onclick = () => formModal("NFS", [["name", "Name"], ["vars", "Vars (JSON: storage_nfs_server, storage_nfs_server_path, external, username, password)", "json"]], (d) => POST("/storage/nfs/", d));
+  $("#ceph").onclick = () => formModal("Ceph", [["name", "Name"], ["vars", "Vars (JSON: monitors, pool, user, key)", "json"]], (d) => POST("/storage/ceph/", d));
+  v.querySelectorAll("[data-dn]").forEach((b) => b.onclick = () => confirmDo("Delete?", () => DEL(`/storage/nfs/${b.dataset.dn}/`)));
+  v.querySelectorAll("[data-dc]").forEach((b) => b.onclick = () => confirmDo("Delete?", () => DEL(`/storage/ceph/${b.dataset.dc}/`)));
+};
+
+views.items = async (v) => {
+  const [items, users] = await Promise.all([GET("/items/"), GET("/users/")]);
+  v.innerHTML = `<h2>Items (projects)</h2><div class="toolbar"><button id="add">Add item</button></div>
+    ${table(items, [["Name", "name"], ["Description", "description"], ["", (i) => `<button class="link" data-mem="${esc(i.name)}">members</button><button class="link" data-res="${esc(i.name)}">resources</button><button class="link" data-del="${esc(i.id)}">delete</button>`]])}
+    <div id="detail"></div>`;
+  $("#add").onclick = () => formModal("Item", [["name", "Name"], ["description", "Description"]], (d) => POST("/items/", d));
+  v.querySelectorAll("[data-del]").forEach((b) => b.onclick = () => confirmDo("Delete item?", () => DEL(`/items/${b.dataset.del}/`)));
+  v.querySelectorAll("[data-mem]").forEach((b) => b.onclick = async () => {
+    const mem = await GET(`/item/profiles/${b.dataset.mem}/`);
+    $("#detail").innerHTML = `<h3>Members of ${esc(b.dataset.mem)}</h3>${table(mem, [["User", "username"], ["Role", "role"]])}<div class="toolbar"><button id="setm" class="secondary">Edit members</button></div>`;
+    $("#setm").onclick = () => formModal("Members", [["profiles", "JSON list of {username, role: VIEWER|MANAGER}", "json"]],
+      (d) => POST(`/item/profiles/${b.dataset.mem}/`, d.profiles), {profiles: mem.map((m) => ({username: m.username, role: m.role}))});
+  });
+  v.querySelectorAll("[data-res]").forEach((b) => b.onclick = async () => {
+    const res = await GET(`/resource/${b.dataset.res}/`);
+    $("#detail").innerHTML = `<h3>Resources of ${esc(b.dataset.res)}</h3>${table(res, [["Type", "resource_type"], ["Id", "resource_id"]])}
+      <div class="toolbar"><button id="addr" class="secondary">Add resources</button></div>`;
+    $("#addr").onclick = () => formModal("Add resources", [["type", "Type", "select", ["CLUSTER", "HOST", "PLAN", "BACKUP_STORAGE", "STORAGE"]], ["ids", "Ids (JSON list)", "json"]],
+      (d) => POST(`/resource/${b.dataset.res}/${d.type}/`, d.ids));
+  });
+  void users;
+};
+
+views.users = crudPage("Users", "/users/", [["Username", "username"], ["Email", "email"], ["Superuser", "is_superuser"], ["Active", "is_active"], ["Source", "source"]],
+  [["username", "Username"], ["email", "Email"], ["password", "Password", "password"], ["is_superuser", "Superuser", "checkbox"], ["is_active", "Active", "checkbox", true]],
+  {extraButtons: `<button class="secondary" onclick="POST('/users/sync/').then(()=>alert('LDAP sync queued'))">Sync LDAP</button>`});
+
+views.settings = async (v, [tab = "system"]) => {
+  const tabs = ["system", "backup-storage", "ldap", "notification"];
+  v.innerHTML = `<h2>Settings</h2><div class="tabs">${tabs.map((t) => `<a href="#/settings/${t}" class="${t === tab ? "active" : ""}">${t}</a>`).join("")}</div><div id="tab"></div>`;
+  const t = $("#tab");
+  if (tab === "backup-storage") return crudPage("Backup storage", "/backupStorage/", [["Name", "name"], ["Type", "type"], ["Region", "region"], ["Status", (b) => st(b.status)]],
+    [["name", "Name"], ["type", "Type", "select", ["S3", "OSS", "AZURE", "LOCAL"]], ["region", "Region"], ["credentials", "Credentials (JSON: bucket, accessKey, secretKey, endpoint | path)", "json"]])(t);
+  const keys = {system: ["local_hostname", "domain_suffix", "ntp_server", "REGISTRY_PREFIX"], ldap: ["AUTH_LDAP_ENABLE", "AUTH_LDAP_SERVER_URI", "AUTH_LDAP_BIND_DN", "AUTH_LDAP_BIND_PASSWORD", "AUTH_LDAP_SEARCH_OU", "AUTH_LDAP_SEARCH_FILTER", "AUTH_LDAP_USER_ATTR_MAP"],
+    notification: ["SMTP_ADDRESS", "SMTP_PORT", "SMTP_USERNAME", "SMTP_PASSWORD", "SMTP_USE_SSL", "DINGTALK_WEBHOOK", "DINGTALK_SECRET", "WORKWEIXIN_CORP_ID", "WORKWEIXIN_AGENT_ID", "WORKWEIXIN_SECRET"]}[tab];
+  const cur = await GET(`/settings?tab=${tab}`);
+  t.innerHTML = `<form id="sf" class="card">${keys.map((k) => `<label>${esc(k)}<input name="${k}" type="${/PASSWORD|SECRET/.test(k) ? "password" : "text"}" value="${esc(cur[k] ?? "")}"></label>`).join("")}
+    <div class="toolbar"><button type="submit">Save</button>${tab === "notification" ? `<button type="button" id="testmail" class="secondary">Test email</button>` : ""}</div><p id="sf-msg" class="muted"></p></form>`;
+  $("#sf").addEventListener("submit", async (e) => {
+    e.preventDefault();
+    const d = Object.fromEntries(new FormData(e.target).entries());
+    for (const k of Object.keys(d)) if (/PASSWORD|SECRET/.test(k) && !d[k]) delete d[k];
+    await api("POST", `/settings?tab=${tab}`, d); $("#sf-msg").textContent = "saved";
+  });
+  if ($("#testmail")) $("#testmail").onclick = async () => { const d = Object.fromEntries(new FormData($("#sf")).entries()); const r = await POST("/notification/email/check/", d); $("#sf-msg").textContent = r.success ? "email sent" : "email failed"; };
+};
+
+views.messages = async (v) => {
+  const [ms, sub, rcv] = await Promise.all([GET("/notification/userMessage/?limit=100"), GET("/notification/subscribe/"), GET("/notification/receiver/")]);
+  v.innerHTML = `<h2>Message center</h2><div class="toolbar"><button id="readall" class="secondary">Mark all read</button><button id="subs" class="secondary">Subscriptions</button><button id="rcv" class="secondary">Receivers</button></div>
+    ${table(ms.results, [["", (m) => m.read_status === "UNREAD" ? "●" : ""], ["Title", (m) => esc(m.message_detail.title)], ["Level", (m) => st(m.message_detail.level)],
+      ["Detail", (m) => esc(JSON.stringify(m.message_detail.content))], ["Date", "date_created"]], "No messages.")}`;
+  $("#readall").onclick = () => PUT("/notification/userMessage/", {ids: null}).then(route);
+  $("#subs").onclick = () => formModal("Subscriptions", [["type", "Type", "select", ["SYSTEM", "CLUSTER"]], ["vars", "Channels (JSON: LOCAL/EMAIL/DINGTALK/WORKWEIXIN: ENABLE|DISABLE)", "json"]],
+    (d) => PUT("/notification/subscribe/", d), sub[0] || {vars: {LOCAL: "ENABLE", EMAIL: "DISABLE", DINGTALK: "DISABLE", WORKWEIXIN: "DISABLE"}});
+  $("#rcv").onclick = () => formModal("Receivers", [["vars", "Addresses (JSON: EMAIL, DINGTALK, WORKWEIXIN)", "json"]], (d) => PUT("/notification/receiver/", d), rcv);
+};
+
+views.logs = async (v) => {
+  v.innerHTML = `<h2>System log</h2><form id="lf" class="toolbar"><select name="level" style="width:auto"><option value="">any level</option><option>INFO</option><option>WARNING</option><option>ERROR</option></select>
+    <input name="keywords" placeholder="keywords" style="width:260px"><input name="days" type="number" value="7" style="width:80px"><button>Search</button></form><div id="lr"></div>`;
+  const run = async () => {
+    const d = Object.fromEntries(new FormData($("#lf")).entries());
+    const r = await POST("/log/", {...d, days: Number(d.days || 7), limit: 200});
+    $("#lr").innerHTML = `<p class="muted">${r.total} entries</p>` + table(r.items, [["Time", "@timestamp"], ["Level", (x) => st(x.levelname)], ["Logger", "name"], ["Message", "msg"]]);
+  };
+  $("#lf").addEventListener("submit", (e) => { e.preventDefault(); run(); });
+  run();
+};
+
+// ------------------------------------------------------------------ navigation
+const NAV = [["Overview", [["dashboard", "Dashboard"], ["clusters", "Clusters"]]],
+  ["Infrastructure", [["hosts", "Hosts"], ["credentials", "Credentials"], ["regions", "Regions"], ["zones", "Zones"], ["plans", "Deploy plans"], ["packages", "Packages"], ["storage", "Storage"]]],
+  ["Administration", [["items", "Items"], ["users", "Users"], ["settings", "Settings"], ["messages", "Messages"], ["logs", "System log"]]]];
+
+function renderNav(current) {
+  $("#nav").innerHTML = NAV.map(([g, items]) => `<div class="group">${g}</div>` + items.filter(([k]) => ME.is_superuser || !["users", "settings", "credentials"].includes(k))
+    .map(([k, label]) => `<a href="#/${k}" class="${k === current ? "active" : ""}">${label}</a>`).join("")).join("");
+}
+
+async function route() {
+  closeSockets();
+  const parts = (location.hash.replace(/^#\/?/, "") || "dashboard").split("/").map(decodeURIComponent);
+  const name = parts[0];
+  renderNav(name === "cluster" || name === "cluster-create" ? "clusters" : name);
+  const view = views[name] || views.dashboard;
+  const v = $("#view");
+  v.innerHTML = `<p class="muted">loading…</p>`;
+  try { await view(v, parts.slice(1)); } catch (e) { v.innerHTML = `<p class="error">${esc(e.message)}</p>`; }
+  GET("/notification/userMessage/unread/").then((r) => { $("#unread").textContent = r.unread; }).catch(() => {});
+}
+
+async function boot() {
+  if (!localStorage.getItem("kop_token")) return showLogin();
+  try { ME = await GET("/profile/"); } catch { return showLogin(); }
+  $("#login").classList.add("hidden");
+  $("#shell").classList.remove("hidden");
+  $("#who").textContent = ME.username;
+  GET("/version/").then((r) => { $("#version").textContent = `v${r.version} · ${r.accelerator}`; });
+  route();
+}
+window.addEventListener("hashchange", route);
+setInterval(refreshToken, 30 * 60 * 1000);
+boot();

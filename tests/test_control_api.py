@@ -68,10 +68,14 @@ def test_cluster_lifecycle_over_http_and_ws(client):
     # worker pool is not running in tests: execute the queued job in-process, then watch the progress socket
     from kubeoperator_amd.control.runtime import jobs
     jobs.run_job(jobs._claim_specific(eid))
-    with client.websocket_connect(f"/ws/progress/{eid}/?interval=0.05") as ws:
+    tok = client.headers["Authorization"].split()[1]
+    with pytest.raises(Exception):
+        with TestClient(create_app()).websocket_connect(f"/ws/progress/{eid}/") as ws:
+            ws.receive_text()
+    with client.websocket_connect(f"/ws/progress/{eid}/?interval=0.05&token={tok}") as ws:
         msg = json.loads(ws.receive_text())
     assert msg["state"] == "SUCCESS" and all(s["status"] == "success" for s in msg["steps"])
-    with client.websocket_connect(f"/ws/tasks/{eid}/log/") as ws:
+    with client.websocket_connect(f"/ws/tasks/{eid}/log/?token={tok}") as ws:
         first = json.loads(ws.receive_text())["message"]
     assert "PLAY" in first or "Start task" in first
     log = client.get(f"/api/v1/tasks/{eid}/log/").json()

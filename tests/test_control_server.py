@@ -88,7 +88,9 @@ def test_progress_websocket(live, control):
     clusters.create_cluster({"name": "demo", "template": "single-master"})
     clusters.add_node("demo", {"name": "m1", "host": "m1", "roles": ["master"]})
     e = deploy.create("demo", "uninstall", run="inline")
-    s = _ws_connect(live, f"/ws/progress/{e['id']}/")
+    from kubeoperator_amd.control.domain import users
+    tok = users.authenticate("admin", "kubeoperator@admin123")["token"]
+    s = _ws_connect(live, f"/ws/progress/{e['id']}/?token={tok}")
     op, data = _ws_recv(s)
     assert op == 1
     msg = json.loads(data)

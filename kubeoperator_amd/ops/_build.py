@@ -102,5 +102,27 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
     return SO_PATH
 
 
+NATIVE_DIR = os.path.join(PKG_DIR, "native")
+
+
+def build_native(force: bool = False) -> list[str]:
+    """Host C++ runtime components (pybind11 modules, no GPU code): ``native/<name>.so``."""
+    import pybind11
+
+    out = []
+    py_inc = sysconfig.get_paths()["include"]
+    for src in sorted(glob.glob(os.path.join(NATIVE_DIR, "*.cpp"))):
+        so = os.path.splitext(src)[0] + ".so"
+        out.append(so)
+        if not force and os.path.exists(so) and os.path.getmtime(so) >= os.path.getmtime(src):
+            continue
+        tmp = so + ".tmp"
+        _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-fvisibility=hidden",
+              "-I", pybind11.get_include(), "-I", py_inc, src, "-o", tmp])
+        os.replace(tmp, so)
+    return out
+
+
 if __name__ == "__main__":
     print(build(verbose=True, force="--force" in sys.argv))
+    print(build_native(force="--force" in sys.argv))

@@ -50,8 +50,8 @@ def main(argv=None) -> int:
     if a.data == "synthetic":
         data = SyntheticTokens(tr.cfg.vocab_size, a.mbs, a.seq, info.device, seed=tc.seed + tr.step, rank=info.rank)
     else:
-        data = TokenFileDataset(a.data, a.mbs, a.seq, info.device, seed=tc.seed + tr.step, rank=info.rank,
-                                world=info.world)
+        data = TokenFileDataset(a.data, a.mbs, a.seq, info.device, seed=tc.seed, rank=info.rank, world=info.world,
+                                start_batch=tr.step * a.accum)
     cuda = info.device.type == "cuda"
     flops_tok = tr.cfg.flops_per_token(a.seq)
     while tr.step < a.steps:

@@ -32,34 +32,57 @@ class SyntheticTokens:
         return [self.next() for _ in range(n)]
 
 
+_M64 = (1 << 64) - 1
+
+
+def _splitmix64(x: int) -> int:
+    x = (x + 0x9E3779B97F4A7C15) & _M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & _M64
+    return x ^ (x >> 31)
+
+
+def window_starts(seed: int, index: int, batch: int, ntok: int, window: int) -> list[int]:
+    """Start offsets of batch ``index`` -- the same function the native prefetcher computes."""
+    span = ntok - window + 1
+    return [_splitmix64((seed & _M64) ^ _splitmix64((index * 0x100000001B3 + r) & _M64)) % span for r in range(batch)]
+
+
 class TokenFileDataset:
+    """Random ``seq_len + 1`` windows of a flat token file; batch ``i`` of rank ``r`` is a pure function of
+    (seed, r, i), so resuming at step ``k`` continues the exact stream (``start_batch = k * grad_accum``)."""
+
     def __init__(self, path: str, micro_batch: int, seq_len: int, device, dtype=np.uint16, seed: int = 0,
-                 rank: int = 0, world: int = 1):
+                 rank: int = 0, world: int = 1, start_batch: int = 0, native: bool = True):
         self.path = path
         self.tokens = np.memmap(path, dtype=dtype, mode="r")
         if len(self.tokens) < seq_len + 2:
             raise ValueError(f"{path}: only {len(self.tokens)} tokens, need > {seq_len + 1}")
         self.B, self.S = micro_batch, seq_len
         self.device = torch.device(device)
-        self.rng = np.random.default_rng(seed * 1000003 + rank)
+        self.seed = seed * 1000003 + rank
         self.rank, self.world = rank, world
+        self.index = start_batch
         self._native = None
-        try:
-            from ..native import prefetch  # type: ignore
+        if native:
+            try:
+                from ..native import prefetch  # type: ignore
 
-            self._native = prefetch.TokenPrefetcher(path, np.dtype(dtype).itemsize, micro_batch, seq_len + 1,
-                                                    seed * 1000003 + rank)
-        except Exception:
-            self._native = None
+                self._native = prefetch.TokenPrefetcher(path, np.dtype(dtype).itemsize, micro_batch, seq_len + 1,
+                                                        self.seed, depth=8, threads=4)
+                if start_batch:
+                    self._native.skip(start_batch)
+            except ImportError:
+                self._native = None
 
     def next(self):
         if self._native is not None:
             arr = self._native.next()
         else:
-            hi = len(self.tokens) - self.S - 1
-            starts = self.rng.integers(0, hi, size=self.B)
+            starts = window_starts(self.seed, self.index, self.B, len(self.tokens), self.S + 1)
             arr = np.stack([np.asarray(self.tokens[s:s + self.S + 1], dtype=np.int64) for s in starts])
-        t = torch.from_numpy(np.asarray(arr, dtype=np.int64))
+        self.index += 1
+        t = torch.from_numpy(arr)
         if self.device.type == "cuda":
             t = t.pin_memory().to(self.device, non_blocking=True)
         return t[:, :-1].contiguous(), t[:, 1:].contiguous()

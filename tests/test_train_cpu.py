@@ -122,3 +122,22 @@ def test_synthetic_data_shapes():
     d = SyntheticTokens(1000, 2, 16, torch.device("cpu"), seed=1, rank=0)
     (ids, tgt), = list(d.batches(1))
     assert ids.shape == (2, 16) and tgt.shape == (2, 16) and int(ids.max()) < 1000
+
+
+def test_native_prefetcher_matches_python_path(tmp_path):
+    import numpy as np
+
+    from kubeoperator_amd.ops._build import build_native
+    from kubeoperator_amd.train.data import TokenFileDataset, write_token_file
+    build_native()
+    path = write_token_file(str(tmp_path / "toks.bin"), np.arange(50_000) % 50_257)
+    nat = TokenFileDataset(path, 3, 128, "cpu", seed=7, rank=1)
+    assert nat._native is not None, "native prefetcher did not load"
+    py = TokenFileDataset(path, 3, 128, "cpu", seed=7, rank=1, native=False)
+    for _ in range(20):
+        (a, at), (b, bt) = nat.next(), py.next()
+        assert torch.equal(a, b) and torch.equal(at, bt)
+        assert torch.equal(a[:, 1:], at[:, :-1])
+    # resume: a fresh loader started at batch 20 continues the same stream
+    res = TokenFileDataset(path, 3, 128, "cpu", seed=7, rank=1, start_batch=20)
+    assert torch.equal(res.next()[0], py.next()[0])

@@ -34,6 +34,8 @@ def main() -> int:
     ap.add_argument("--dp", default="allreduce", choices=["allreduce", "zero1"])
     ap.add_argument("--bucket-mb", type=int, default=512)
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--gemm-tuning", default="use", choices=["off", "use", "tune"],
+                    help="hipBLASLt solution selection: committed TunableOp winners (use), heuristic (off), re-tune")
     args = ap.parse_args()
 
     import torch
@@ -42,6 +44,9 @@ def main() -> int:
     from kubeoperator_amd.train import SyntheticTokens, TrainConfig, Trainer
 
     info = init_distributed(args.device)
+    from kubeoperator_amd.train import gemm_tuning
+
+    tuning = gemm_tuning.setup(args.gemm_tuning, rank=info.rank)
     world = info.world
     if world != args.gpus and info.is_main:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the real world size",
@@ -70,6 +75,7 @@ def main() -> int:
     sync()
     elapsed = time.perf_counter() - t0
     elapsed = all_reduce_max(elapsed, info)
+    gemm_tuning.finish(tuning, info.rank)
     last_loss = float(loss.item()) if loss is not None else float("nan")
     tokens = world * trainer.tokens_per_step * args.steps
     value = tokens / elapsed
@@ -107,6 +113,7 @@ def main() -> int:
             "last_loss": round(last_loss, 4),
             "peak_mem_gb_rank0": round(mem_gb, 1),
             "setup_s": round(trainer.setup_seconds, 1),
+            "gemm_selection": tuning,
         }
         print(json.dumps(out), flush=True)
     shutdown(info)

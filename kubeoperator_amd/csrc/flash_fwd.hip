@@ -203,6 +203,256 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_fwd_kernel(const bf16_t* __rest
   }
 }
 
+// ------------------------------------------------------------------------------------------------------
+// 8-wave forward: one 512-thread workgroup = 256 query rows (8 waves x 32) of one (b, q-head), so every
+// K/V tile fetched into LDS serves twice the query rows of the 4-wave kernel, and the two waves sharing a
+// SIMD (w and w+4) belong to ONE workgroup, where their phases can be arranged:
+//   * STAGGER: waves 4-7 run half a tile behind -- in the interval of tile t they do softmax + P.V of tile
+//     t-1 and then Q.K^T of tile t (keeping S^T in registers across the barrier), while waves 0-3 do
+//     Q.K^T, softmax and P.V of tile t. Each SIMD then pairs one wave's MFMA phase with the other's VALU
+//     (softmax) phase instead of running both in lockstep (guide: MI355X_MICROARCH "Two waves per SIMD",
+//     item 9). The ring has 4 slots so the late half can still read V(t-1) while t+2 is being fetched.
+//   * one barrier per tile (the ring is deep enough that a slot is refilled only after every wave has
+//     passed the barrier that follows its last read);
+//   * V^T fragments for the next 32-column block are read (ds_read_b64_tr_b16) while the current block's
+//     MFMAs run, retired by counted lgkmcnt waits; the first block's reads fly under the softmax.
+template <int D, bool STAGGER>
+__global__ void __launch_bounds__(512, 1) fa_fwd8_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
+                                                         const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
+                                                         float* __restrict__ lse, int B, int S, int Hq, int Hkv,
+                                                         int64_t qs, int64_t ks, int64_t vs, int64_t os,
+                                                         float scale_log2, int causal) {
+  constexpr int NW = 8, BM = 256, BN = 64, ROWB = D * 2;
+  constexpr int TILE = BN * ROWB;
+  constexpr int NSLOT = STAGGER ? 4 : 3;
+  constexpr int SLOTS = ROWB / 16, RPP = 1024 / ROWB;
+  constexpr int PPW = (TILE / 1024) / NW;  // DMA pieces per wave per tile, each of K and V
+  static_assert(PPW >= 1 && PPW * NW * 1024 == TILE, "tile must split evenly over the waves");
+  constexpr int DT = D / 32;                // 32-column output blocks
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+#define KBUF(sl) (smem + (sl) * 2 * TILE)
+#define VBUF(sl) (smem + (sl) * 2 * TILE + TILE)
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hh = lane >> 5;
+  const bool late = STAGGER && wid >= 4;
+  const int nqb = S / BM;
+  const int nwork = B * Hq * nqb;
+  const int work = xcd_remap(blockIdx.x, nwork);
+  const int qb = causal ? (nqb - 1 - work / (B * Hq)) : work / (B * Hq);
+  const int rest = work % (B * Hq);
+  const int b = rest / Hq, hq = rest % Hq;
+  const int kvh = hq / (Hq / Hkv);
+  const int q0 = qb * BM, q0w = q0 + wid * 32;
+  const int ntiles = causal ? (q0 + BM) / BN : S / BN;
+
+  const bf16_t* kbase = k + (int64_t)(b * S) * ks + kvh * D;
+  const bf16_t* vbase = v + (int64_t)(b * S) * vs + kvh * D;
+  const int prow = lane / SLOTS, pslot = lane % SLOTS;
+  auto issue = [&](int t) {
+    const int sl = t % NSLOT;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int piece = wid * PPW + i;
+      const int row = piece * RPP + prow;
+      const int ch = pslot ^ swz_xor<ROWB>(row);
+      glds16(kbase + (int64_t)(t * BN + row) * ks + ch * 8, KBUF(sl) + piece * 1024);
+      glds16(vbase + (int64_t)(t * BN + row) * vs + ch * 8, VBUF(sl) + piece * 1024);
+    }
+  };
+  issue(0);
+  if (ntiles > 1) issue(1);
+
+  bf16x8 qf[D / 16];
+  {
+    const bf16_t* qp = q + (int64_t)(b * S + q0w + r) * qs + hq * D + 8 * hh;
+#pragma unroll
+    for (int kk = 0; kk < D / 16; ++kk) qf[kk] = *reinterpret_cast<const bf16x8*>(qp + 16 * kk);
+#pragma unroll
+    for (int kk = 0; kk < D / 16; ++kk) asm volatile("" : "+v"(qf[kk]));
+  }
+  f32x16 oacc[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) oacc[i] = f32x16{0};
+  float m = -INFINITY, l = 0.f;
+  const int tq = (lane & 15) >> 2, tp = lane & 3, tg1 = (lane >> 4) & 1;
+  if (wid >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the second-dispatched half (T5)
+
+  // S^T = K . Q^T for the 64 keys of tile t (two 32-key accumulators), causal mask applied
+  auto qk = [&](int t, f32x16& s0, f32x16& s1) {
+    const char* Kb = KBUF(t % NSLOT);
+    s0 = f32x16{0};
+    s1 = f32x16{0};
+    bf16x8 ka = lds_read8(Kb + swz<ROWB>(r, hh));
+    bf16x8 kb = lds_read8(Kb + swz<ROWB>(32 + r, hh));
+#pragma unroll
+    for (int kk = 0; kk < D / 16; ++kk) {
+      bf16x8 na, nb;
+      if (kk + 1 < D / 16) {
+        na = lds_read8(Kb + swz<ROWB>(r, 2 * (kk + 1) + hh));
+        nb = lds_read8(Kb + swz<ROWB>(32 + r, 2 * (kk + 1) + hh));
+      }
+      s0 = mfma32(ka, qf[kk], s0);
+      s1 = mfma32(kb, qf[kk], s1);
+      if (kk + 1 < D / 16) {
+        ka = na;
+        kb = nb;
+      }
+    }
+    const int kv0 = t * BN;
+    if (causal && kv0 + BN - 1 > q0w) {
+      const int qi = q0w + r;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int key = kv0 + (j & 3) + 8 * (j >> 2) + 4 * hh;
+        if (key > qi) s0[j] = -INFINITY;
+        if (key + 32 > qi) s1[j] = -INFINITY;
+      }
+    }
+  };
+  // V^T fragments of output block dt (8 transposed reads, retired by the caller's counted wait)
+  auto vread = [&](const char* Vb, int dt, bf16x4* t) {
+    const int col = dt * 32 + 16 * tg1 + 4 * tp;
+    const int ch = col >> 3, bo = (col & 7) * 2;
+#pragma unroll
+    for (int ks4 = 0; ks4 < 4; ++ks4) {
+      const int rowA = (ks4 >> 1) * 32 + 16 * (ks4 & 1) + 4 * hh + tq;
+      t[2 * ks4] = lds_tr_read_asm(Vb + swz<ROWB>(rowA, ch) + bo);
+      t[2 * ks4 + 1] = lds_tr_read_asm(Vb + swz<ROWB>(rowA + 8, ch) + bo);
+    }
+  };
+  // online softmax of tile t's scores and O^T += V^T . P^T
+  auto softmax_pv = [&](int t, f32x16& s0, f32x16& s1, auto db_tag) {
+    constexpr bool DB = decltype(db_tag)::value;  // double-buffered V^T reads (needs 16 more VGPRs)
+    const char* Vb = VBUF(t % NSLOT);
+    bf16x4 ta[8], tb[DB ? 8 : 1];
+    vread(Vb, 0, ta);  // flies under the softmax
+    float mx = fmaxf(s0[0], s1[0]);
+#pragma unroll
+    for (int j = 1; j < 16; ++j) mx = fmaxf(mx, fmaxf(s0[j], s1[j]));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mt = mx * scale_log2;
+    if (__any(mt > m + 8.f)) {
+      const float mnew = fmaxf(m, mt);
+      const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+      m = mnew;
+      l *= alpha;
+#pragma unroll
+      for (int i = 0; i < DT; ++i) oacc[i] *= alpha;
+    }
+    float ls = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      s0[j] = __builtin_amdgcn_exp2f(fmaf(s0[j], scale_log2, -m));
+      s1[j] = __builtin_amdgcn_exp2f(fmaf(s1[j], scale_log2, -m));
+      ls += s0[j] + s1[j];
+    }
+    l += ls;
+    bf16x8 pf[4];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const uint32_t a = pack2(s0[8 * s + j], s0[8 * s + j + 1]);
+        const uint32_t c = pack2(s1[8 * s + j], s1[8 * s + j + 1]);
+        pf[s][j] = (short)(a & 0xffff);
+        pf[s][j + 1] = (short)(a >> 16);
+        pf[2 + s][j] = (short)(c & 0xffff);
+        pf[2 + s][j + 1] = (short)(c >> 16);
+      }
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      bf16x4* cur = (DB && (dt & 1)) ? tb : ta;
+      bf16x4* nxt = (DB && (dt & 1)) ? ta : tb;
+      if (!DB) {
+        if (dt > 0) vread(Vb, dt, cur);
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]), "+v"(cur[4]), "+v"(cur[5]),
+                       "+v"(cur[6]), "+v"(cur[7]));
+      } else if (dt + 1 < DT) {
+        vread(Vb, dt + 1, nxt);
+        asm volatile("s_waitcnt lgkmcnt(8)"
+                     : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]), "+v"(cur[4]), "+v"(cur[5]),
+                       "+v"(cur[6]), "+v"(cur[7]));
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]), "+v"(cur[4]), "+v"(cur[5]),
+                       "+v"(cur[6]), "+v"(cur[7]));
+      }
+#pragma unroll
+      for (int ks4 = 0; ks4 < 4; ++ks4) oacc[dt] = mfma32(cat44(cur[2 * ks4], cur[2 * ks4 + 1]), pf[ks4], oacc[dt]);
+    }
+  };
+
+  const int nloop = ntiles + (STAGGER ? 1 : 0);
+  // every wave executes the same number of barriers; the two halves run separate loops so each loop's
+  // live ranges are allocated on their own (one merged body spills)
+  auto top = [&](int it) {
+    if (it < ntiles) {
+      if (it + 1 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (it + 2 < ntiles) issue(it + 2);
+  };
+  if (late) {
+    f32x16 sp0, sp1;  // scores of the pending tile, carried across the barrier
+    bool pending = false;
+    for (int it = 0; it < nloop; ++it) {
+      top(it);
+      if (pending) softmax_pv(it - 1, sp0, sp1, std::false_type{});
+      pending = it < ntiles && (!causal || it * BN <= q0w + 31);
+      if (pending) qk(it, sp0, sp1);
+      asm volatile("" ::: "memory");
+    }
+  } else {
+    for (int it = 0; it < nloop; ++it) {
+      top(it);
+      if (it < ntiles && (!causal || it * BN <= q0w + 31)) {
+        f32x16 s0, s1;
+        qk(it, s0, s1);
+        softmax_pv(it, s0, s1, std::true_type{});
+      }
+      asm volatile("" ::: "memory");
+    }
+  }
+#undef KBUF
+#undef VBUF
+
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = 1.f / lt;
+  if (hh == 0) lse[((int64_t)(b * Hq + hq)) * S + q0w + r] = (m + __log2f(lt)) * 0.69314718056f;
+  bf16_t* op = o + (int64_t)(b * S + q0w + r) * os + hq * D;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      u32x2 w;
+      w[0] = pack2(oacc[dt][4 * g4] * inv, oacc[dt][4 * g4 + 1] * inv);
+      w[1] = pack2(oacc[dt][4 * g4 + 2] * inv, oacc[dt][4 * g4 + 3] * inv);
+      *reinterpret_cast<u32x2*>(op + dt * 32 + 8 * g4 + 4 * hh) = w;
+    }
+  }
+}
+
+template <int D, bool STAGGER>
+static void launch_fwd8(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int S,
+                        int Hq, int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t os, float sl2, bool causal,
+                        hipStream_t stream) {
+  const size_t lds = (STAGGER ? 4 : 3) * 2 * 64 * (D * 2);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)fa_fwd8_kernel<D, STAGGER>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    attr = true;
+  }
+  const int grid = B * Hq * (S / 256);
+  fa_fwd8_kernel<D, STAGGER><<<grid, 512, lds, stream>>>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal);
+}
+
 constexpr int kFwdWaves = 4;
 
 template <int D>
@@ -226,6 +476,20 @@ int flash_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o,
   if (S % (32 * kFwdWaves) != 0 || Hq % Hkv != 0) return -1;
   if (qs % 8 || ks % 8 || vs % 8 || os % 8) return -2;
   const float sl2 = scale * 1.4426950408889634f;
+  static const int variant = [] {
+    const char* e = getenv("KOP_FWD_VARIANT");
+    return e ? atoi(e) : 9;
+  }();
+  if (S % 256 == 0 && variant >= 8) {
+    if (D == 128) {
+      if (variant == 9) launch_fwd8<128, true>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
+      else launch_fwd8<128, false>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
+    } else if (D == 64) {
+      if (variant == 9) launch_fwd8<64, true>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
+      else launch_fwd8<64, false>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
+    } else return -3;
+    return 0;
+  }
   if (D == 128) launch_fwd<128>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
   else if (D == 64) launch_fwd<64>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
   else return -3;

@@ -1,0 +1,283 @@
+"""Day-2 / auxiliary control-plane paths: AUTOMATIC (IaaS) clusters with IP pools, Terraform rendering,
+scale out/in and destroy; the periodic scheduler; S3 backup storage against a local SigV4-checking stub;
+cluster monitoring (data blob with AMD GPU metrics, events -> messages, health, grade) with stub clients."""
+import datetime as dt
+import hashlib
+import http.server
+import json
+import os
+import threading
+
+import pytest
+
+from kubeoperator_amd.control.domain import backup, cloud, clusters, deploy, messages, monitor
+from kubeoperator_amd.control.store import models as M
+from kubeoperator_amd.control.store.db import session_scope
+
+
+# ------------------------------------------------------------------------------------------------ IaaS
+def _plan(provider="fake", n_ips=20, template="SINGLE"):
+    with session_scope() as s:
+        tmpl = s.query(M.CloudProviderTemplate).filter_by(name=provider).first()
+        r = M.Region(name="r1", cloud_region="dc1", template_id=tmpl.id if tmpl else None,
+                     vars={"provider": provider, "vc_host": "vc.local", "vc_username": "u", "vc_password": "p",
+                           "datacenter": "dc1"})
+        s.add(r)
+        s.flush()
+        z1 = M.Zone(name="z1", region_id=r.id, cloud_zone="cluster-a",
+                    vars={"ip_start": "10.1.0.10", "ip_end": f"10.1.0.{9 + n_ips // 2}", "net_mask": "255.255.255.0",
+                          "gateway": "10.1.0.1", "dns1": "10.1.0.2", "provider": provider, "cluster": "cluster-a",
+                          "datastore": "ds1", "network": "vm-net", "image_name": "ubuntu-22.04-rocm"})
+        z2 = M.Zone(name="z2", region_id=r.id, cloud_zone="cluster-b",
+                    vars={"ip_start": "10.2.0.10", "ip_end": f"10.2.0.{9 + n_ips // 2}", "net_mask": "255.255.255.0",
+                          "gateway": "10.2.0.1", "dns1": "10.2.0.2", "provider": provider, "cluster": "cluster-b",
+                          "datastore": "ds1", "network": "vm-net", "image_name": "ubuntu-22.04-rocm"})
+        s.add_all([z1, z2])
+        s.flush()
+        p = M.Plan(name="p1", region_id=r.id, zone_ids=[z1.id, z2.id], deploy_template=template,
+                   vars={"master_model": "large", "worker_model": "mi355x-8gpu"})
+        s.add(p)
+        s.flush()
+        return p.id, z1.id, z2.id
+
+
+def test_ip_pool_and_allocation(control):
+    _, z1, _ = _plan(n_ips=4)
+    got = {cloud.allocate_ip(z1), cloud.allocate_ip(z1)}
+    assert got == {"10.1.0.10", "10.1.0.11"}
+    cloud.recover_ip(z1, "10.1.0.10")
+    assert cloud.allocate_ip(z1) == "10.1.0.10"
+
+
+def test_automatic_cluster_install_scale_destroy(control):
+    pid, z1, z2 = _plan()
+    clusters.create_cluster({"name": "auto", "template": "single-master", "deploy_type": "AUTOMATIC", "plan": pid,
+                             "worker_size": 2, "cluster_doamin_suffix": "lab.local"})
+    e = deploy.create("auto", "install", run="inline")
+    assert e["state"] == "SUCCESS", e["result_summary"].get("dark")
+    assert e["steps"][0]["name"] == "create-resource"
+    nodes = sorted(n["name"] for n in clusters.list_nodes("auto"))
+    assert nodes == ["master1.auto.lab.local", "worker1.auto.lab.local", "worker2.auto.lab.local"]
+    tf = open(os.path.join(control.cfg.data_dir, "terraform", "auto", "main.tf")).read()
+    assert "worker2" in tf and "10.1.0." in tf
+    with session_scope() as s:
+        ips = {h.name: h.ip for h in s.query(M.Host)}
+    assert ips["worker1.auto.lab.local"].startswith("10.2.") or ips["worker1.auto.lab.local"].startswith("10.1.")
+    # multi-AZ round robin: the two workers land in different zones
+    assert ips["worker1.auto.lab.local"].split(".")[1] != ips["worker2.auto.lab.local"].split(".")[1]
+
+    e = deploy.create("auto", "scale", {"num": 3}, run="inline")
+    assert e["state"] == "SUCCESS", e["result_summary"].get("dark")
+    assert len(clusters.list_nodes("auto")) == 4
+    e = deploy.create("auto", "scale", {"num": 1}, run="inline")
+    assert e["state"] == "SUCCESS"
+    assert len(clusters.list_nodes("auto")) == 2
+
+    e = deploy.create("auto", "uninstall", run="inline")
+    assert e["state"] == "SUCCESS"
+    assert clusters.list_nodes("auto") == []
+    with session_scope() as s:
+        assert all(not z.ip_used for z in s.query(M.Zone))
+
+
+def test_capacity_check(control):
+    pid, _, _ = _plan(n_ips=2)
+    clusters.create_cluster({"name": "big", "template": "single-master", "deploy_type": "AUTOMATIC", "plan": pid,
+                             "worker_size": 5})
+    with pytest.raises(Exception):
+        deploy.create("big", "scale", {"num": 10}, run="none")
+
+
+@pytest.mark.parametrize("provider", ["vsphere", "openstack"])
+def test_terraform_templates_render(control, provider):
+    hosts = [{"name": "master1.c.local", "short_name": "master1", "role": "master", "ip": "10.0.0.5", "cpu": 8,
+              "memory": 32768, "gpu": 0, "gpu_model": "", "zone": {"cluster": "a", "datastore": "d", "network": "n",
+                                                                    "net_mask": "255.255.255.0", "gateway": "10.0.0.1",
+                                                                    "dns1": "10.0.0.2", "image_name": "img",
+                                                                    "zone_name": "z1", "key": "z1", "name": "a",
+                                                                    "network_id": "net", "floating_network": "pub"},
+              "zone_name": "z1", "domain": "c.local"}]
+    variables = {"vc_host": "vc", "vc_username": "u", "vc_password": "p", "datacenter": "dc", "region": "r",
+                 "auth_url": "http://keystone:5000/v3", "username": "u", "password": "p", "project_name": "p",
+                 "user_domain": "Default", "project_domain": "Default", "flavor": "m1.xlarge", "image_name": "img"}
+    variables["zones"] = [hosts[0]["zone"]]
+    path = cloud.render_terraform("c", provider, variables, hosts)
+    text = open(path).read()
+    assert "master1" in text and "10.0.0.5" in text
+
+
+# ------------------------------------------------------------------------------------------------ scheduler
+def test_cron_and_due(control):
+    from kubeoperator_amd.control.runtime import scheduler
+    t = dt.datetime(2026, 10, 15, 1, 0)
+    assert scheduler.cron_match("0 1 * * *", t)
+    assert not scheduler.cron_match("0 2 * * *", t)
+    assert scheduler.cron_match("*/15 * * * *", t.replace(minute=45))
+    assert scheduler.cron_match("0 0-3 * * 1-5", t)  # Thursday
+    scheduler.seed_defaults()
+    fired = {n for n, _, _ in scheduler.due(t)}
+    assert {"cluster-backup-daily", "save-cluster-data", "host-health-check"} <= fired
+    again = {n for n, _, _ in scheduler.due(t + dt.timedelta(seconds=30))}
+    assert "cluster-backup-daily" not in again and "save-cluster-data" not in again
+    later = {n for n, _, _ in scheduler.due(t + dt.timedelta(minutes=6))}
+    assert "save-cluster-data" in later
+
+
+def test_scheduler_tick_submits_jobs(control):
+    from kubeoperator_amd.control.domain import tasks  # noqa: F401  (registers jobs)
+    from kubeoperator_amd.control.runtime import jobs, scheduler
+    scheduler.seed_defaults()
+    fired = scheduler.Scheduler().tick(dt.datetime(2026, 10, 15, 1, 0))
+    assert "cluster-backup-daily" in fired
+    with session_scope() as s:
+        names = {j.name for j in s.query(M.Job)}
+    assert "cluster_backup_all" in names
+    pool = jobs.WorkerPool(concurrency=2, poll_s=0.05).start()
+    try:
+        for _ in range(200):
+            with session_scope() as s:
+                if all(j.state in ("SUCCESS", "FAILURE") for j in s.query(M.Job)):
+                    break
+            import time
+            time.sleep(0.05)
+    finally:
+        pool.stop()
+    with session_scope() as s:
+        assert all(j.state == "SUCCESS" for j in s.query(M.Job)), [(j.name, j.result) for j in s.query(M.Job)]
+
+
+# ------------------------------------------------------------------------------------------------ S3 backup
+class _S3Stub(http.server.BaseHTTPRequestHandler):
+    store = {}
+
+    def _ok_sig(self):
+        auth = self.headers.get("Authorization", "")
+        body_hash = self.headers.get("x-amz-content-sha256", "")
+        return auth.startswith("AWS4-HMAC-SHA256 Credential=AK/") and "Signature=" in auth and len(body_hash) == 64
+
+    def do_PUT(self):
+        n = int(self.headers.get("Content-Length", 0))
+        data = self.rfile.read(n)
+        if not self._ok_sig() or hashlib.sha256(data).hexdigest() != self.headers["x-amz-content-sha256"]:
+            self.send_response(403)
+            self.end_headers()
+            return
+        self.store[self.path] = data
+        self.send_response(200)
+        self.end_headers()
+
+    def do_GET(self):
+        if self.path not in self.store:
+            self.send_response(404)
+            self.end_headers()
+            return
+        self.send_response(200)
+        self.send_header("Content-Length", str(len(self.store[self.path])))
+        self.end_headers()
+        self.wfile.write(self.store[self.path])
+
+    def do_HEAD(self):
+        self.send_response(200 if self.path in self.store or self.path.count("/") == 1 else 404)
+        self.end_headers()
+
+    def do_DELETE(self):
+        self.store.pop(self.path, None)
+        self.send_response(204)
+        self.end_headers()
+
+    def log_message(self, *a):
+        pass
+
+
+def test_s3_storage_roundtrip(tmp_path):
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), _S3Stub)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    try:
+        st = backup.S3Storage("AK", "SK", "bkt", "us-east-1", f"http://127.0.0.1:{srv.server_port}")
+        src = tmp_path / "a.zip"
+        src.write_bytes(b"PK" + os.urandom(1000))
+        st.upload(str(src), "demo/a.zip")
+        assert st.exists("demo/a.zip") and st.check()
+        st.download("demo/a.zip", str(tmp_path / "b.zip"))
+        assert (tmp_path / "b.zip").read_bytes() == src.read_bytes()
+        st.delete("demo/a.zip")
+        assert not st.exists("demo/a.zip")
+    finally:
+        srv.shutdown()
+
+
+def test_backup_retention(control, tmp_path):
+    clusters.create_cluster({"name": "c", "template": "single-master"})
+    c = clusters.get_cluster("c")
+    with session_scope() as s:
+        st = M.BackupStorage(name="l", type="LOCAL", credentials={"path": str(tmp_path / "bk")})
+        s.add(st)
+        s.flush()
+        for i in range(5):
+            s.add(M.ClusterBackup(name=f"c-{i}.zip", cluster_id=c.id, backup_storage_id=st.id,
+                                  date_created=dt.datetime(2026, 1, 1 + i)))
+    removed = backup.apply_retention(c.id, 2)
+    assert len(removed) == 3
+    with session_scope() as s:
+        assert sorted(b.name for b in s.query(M.ClusterBackup)) == ["c-3.zip", "c-4.zip"]
+
+
+# ------------------------------------------------------------------------------------------------ monitor
+class _K8s:
+    def get(self, path, params=None):
+        if path == "/api/v1/nodes":
+            return {"items": [{"metadata": {"name": "w1"}, "status": {
+                "addresses": [{"type": "InternalIP", "address": "10.0.0.2"}],
+                "allocatable": {"amd.com/gpu": "8"}, "capacity": {"amd.com/gpu": "8"},
+                "conditions": [{"type": "Ready", "status": "True"}], "nodeInfo": {"kubeletVersion": "v1.30.6"}}}]}
+        if path == "/api/v1/pods":
+            return {"items": [{"metadata": {"name": "p1", "namespace": "default"},
+                               "status": {"phase": "Failed", "containerStatuses": [{"restartCount": 3}]}}]}
+        if path == "/api/v1/namespaces":
+            return {"items": [{"metadata": {"name": "default"}, "status": {"phase": "Active"}}]}
+        if path in ("/apis/apps/v1/deployments", "/apis/apps/v1/daemonsets"):
+            return {"items": [{"kind": "Deployment", "metadata": {"name": "train", "namespace": "ml"},
+                               "spec": {"template": {"spec": {"containers": [{
+                                   "name": "trainer", "image": "kop/train:latest",
+                                   "resources": {"requests": {"amd.com/gpu": 8}}}]}}}}]}
+        if path == "/api/v1/events":
+            return {"items": [{"metadata": {"uid": "e1", "namespace": "ml"}, "type": "Warning", "reason": "OOMKilled",
+                               "message": "container trainer OOM", "involvedObject": {"kind": "Pod", "name": "p1"},
+                               "lastTimestamp": "2026-10-15T01:00:00Z"}]}
+        if path == "/api/v1/componentstatuses":
+            return {"items": []}
+        return {}
+
+
+class _Prom:
+    def scalar(self, q, default=0.0):
+        if "gpu_gfx_activity" in q and q.startswith("avg"):
+            return 87.0
+        if "count(gpu_gfx_activity" in q:
+            return 8
+        if "mem" in q.lower():
+            return 0.5
+        return 0.25
+
+
+def test_monitor_with_stub_clients(control):
+    clusters.create_cluster({"name": "mon", "template": "single-master"})
+    monitor.set_clients("mon", k8s=_K8s(), prom=_Prom())
+    d = monitor.set_cluster_data("mon")
+    assert d["gpu_total"] == 8 and d["gpu_allocatable"] == 8
+    assert d["nodes"][0]["gpu_util"] == pytest.approx(0.87) and d["nodes"][0]["gpu_count"] == 8
+    assert d["error_pods"][0]["name"] == "p1" and d["restart_pods"]
+    assert monitor.get_cluster_data("mon")["name"] == "mon"
+    assert monitor.save_events("mon") == 1
+    assert monitor.save_events("mon") == 0  # dedup by uid
+    ev = monitor.search_events("mon", type_="Warning")
+    assert ev["total"] == 1 and ev["items"][0]["reason"] == "OOMKilled"
+    with session_scope() as s:
+        assert s.query(M.Message).filter(M.Message.level == "WARNING").count() >= 1
+    h = monitor.cluster_health("mon")
+    assert h["available_rate"] == pytest.approx(25.0)
+    g = monitor.grade("mon")
+    ids = {r["id"] for r in g["results"][0]["results"] if not r["success"]}
+    assert {"tagNotSpecified", "gpuLimitMissing", "livenessProbeMissing"} <= ids
+    monitor.record_availability("mon", 99.0)
+    assert monitor.availability_history(clusters.get_cluster("mon").id)[0]["available_rate"] == 99.0

@@ -371,6 +371,185 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dq_kernel(
   }
 }
 
+// 8-wave dQ: 512 threads = 256 query rows of one (b, q-head), same K/V tile stream and staggered halves as
+// fa_fwd8_kernel (flash_fwd.hip): waves 4-7 run half a tile behind (dS + dQ MFMAs of tile t-1, then the
+// S^T / dP^T MFMAs of tile t, carried across the barrier), 4-slot LDS ring, one barrier per tile.
+template <int D, bool STAGGER>
+__global__ void __launch_bounds__(512, 1) fa_bwd_dq8_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
+    bf16_t* __restrict__ dq, int B, int S, int Hq, int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t dos,
+    int64_t dqs, float scale, int causal) {
+  constexpr int NW = 8, BM = 256, BN = 64, ROWB = D * 2;
+  constexpr int TILE = BN * ROWB;
+  constexpr int NSLOT = STAGGER ? 4 : 3;
+  constexpr int PPW = (TILE / 1024) / NW;
+  static_assert(PPW >= 1 && PPW * NW * 1024 == TILE, "tile must split evenly over the waves");
+  constexpr int DT = D / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+#define KBUF(sl) (smem + (sl) * 2 * TILE)
+#define VBUF(sl) (smem + (sl) * 2 * TILE + TILE)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hh = lane >> 5;
+  const int tq = (lane & 15) >> 2, tp = lane & 3, tg1 = (lane >> 4) & 1;
+  const bool late = STAGGER && wid >= 4;
+  const int nqb = S / BM;
+  const int nwork = B * Hq * nqb;
+  const int work = xcd_remap(blockIdx.x, nwork);
+  const int qb = causal ? (nqb - 1 - work / (B * Hq)) : work / (B * Hq);
+  const int rest = work % (B * Hq);
+  const int b = rest / Hq, hq = rest % Hq;
+  const int kvh = hq / (Hq / Hkv);
+  const int q0 = qb * BM, q0w = q0 + wid * 32;
+  const int ntiles = causal ? (q0 + BM) / BN : S / BN;
+  const float c2 = scale * 1.4426950408889634f;
+
+  const bf16_t* kbase = k + (int64_t)(b * S) * ks + kvh * D;
+  const bf16_t* vbase = v + (int64_t)(b * S) * vs + kvh * D;
+  auto issue = [&](int t) {
+    dma_tile<ROWB, NW, BN>(KBUF(t % NSLOT), kbase + (int64_t)(t * BN) * ks, ks, wid, lane);
+    dma_tile<ROWB, NW, BN>(VBUF(t % NSLOT), vbase + (int64_t)(t * BN) * vs, vs, wid, lane);
+  };
+  issue(0);
+  if (ntiles > 1) issue(1);
+
+  const int qi = q0w + r;
+  bf16x8 qf[D / 16], of[D / 16];
+  float lse2, dl;
+  {
+    const bf16_t* qp = q + (int64_t)(b * S + qi) * qs + hq * D + 8 * hh;
+    const bf16_t* op = dout + (int64_t)(b * S + qi) * dos + hq * D + 8 * hh;
+#pragma unroll
+    for (int kk = 0; kk < D / 16; ++kk) {
+      qf[kk] = *reinterpret_cast<const bf16x8*>(qp + 16 * kk);
+      of[kk] = *reinterpret_cast<const bf16x8*>(op + 16 * kk);
+    }
+    lse2 = lse[((int64_t)(b * Hq + hq)) * S + qi] * 1.4426950408889634f;
+    dl = delta[((int64_t)(b * Hq + hq)) * S + qi];
+#pragma unroll
+    for (int kk = 0; kk < D / 16; ++kk) asm volatile("" : "+v"(qf[kk]), "+v"(of[kk]));
+    asm volatile("" : "+v"(lse2), "+v"(dl));
+  }
+  f32x16 dqacc[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) dqacc[i] = f32x16{0};
+  if (wid >= 4) __builtin_amdgcn_s_setprio(1);
+
+  // S^T = K.Q^T and dP^T = V.dO^T for the 64 keys of tile t
+  auto scores = [&](int t, f32x16& s0, f32x16& s1, f32x16& p0, f32x16& p1) {
+    const char* Kb = KBUF(t % NSLOT);
+    const char* Vb = VBUF(t % NSLOT);
+    s0 = s1 = p0 = p1 = f32x16{0};
+#pragma unroll
+    for (int kk = 0; kk < D / 16; ++kk) {
+      const bf16x8 ka = lds_read8(Kb + swz<ROWB>(r, 2 * kk + hh));
+      const bf16x8 kb = lds_read8(Kb + swz<ROWB>(32 + r, 2 * kk + hh));
+      const bf16x8 va = lds_read8(Vb + swz<ROWB>(r, 2 * kk + hh));
+      const bf16x8 vb = lds_read8(Vb + swz<ROWB>(32 + r, 2 * kk + hh));
+      s0 = mfma32(ka, qf[kk], s0);
+      s1 = mfma32(kb, qf[kk], s1);
+      p0 = mfma32(va, of[kk], p0);
+      p1 = mfma32(vb, of[kk], p1);
+    }
+  };
+  auto kread = [&](const char* Kb, int dt, bf16x4* t) {
+    const int col = dt * 32 + 16 * tg1 + 4 * tp;
+    const int ch = col >> 3, bo = (col & 7) * 2;
+#pragma unroll
+    for (int ks4 = 0; ks4 < 4; ++ks4) {
+      const int rowA = (ks4 >> 1) * 32 + 16 * (ks4 & 1) + 4 * hh + tq;
+      t[2 * ks4] = lds_tr_read_asm(Kb + swz<ROWB>(rowA, ch) + bo);
+      t[2 * ks4 + 1] = lds_tr_read_asm(Kb + swz<ROWB>(rowA + 8, ch) + bo);
+    }
+  };
+  // dS^T = P^T (dP^T - delta) and dQ^T += K^T . dS^T
+  auto grad = [&](int t, f32x16& s0, f32x16& s1, f32x16& p0, f32x16& p1) {
+    const char* Kb = KBUF(t % NSLOT);
+    bf16x4 ta[8];
+    kread(Kb, 0, ta);  // flies under the dS VALU work
+    const int kv0 = t * BN;
+    const bool diag = causal && kv0 + BN - 1 > q0w;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int key = kv0 + (j & 3) + 8 * (j >> 2) + 4 * hh;
+      float pa = __builtin_amdgcn_exp2f(fmaf(s0[j], c2, -lse2));
+      float pb = __builtin_amdgcn_exp2f(fmaf(s1[j], c2, -lse2));
+      if (diag && key > qi) pa = 0.f;
+      if (diag && key + 32 > qi) pb = 0.f;
+      s0[j] = pa * (p0[j] - dl);
+      s1[j] = pb * (p1[j] - dl);
+    }
+    bf16x8 sf[4];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const uint32_t a = pack2(s0[8 * s + j], s0[8 * s + j + 1]);
+        const uint32_t c = pack2(s1[8 * s + j], s1[8 * s + j + 1]);
+        sf[s][j] = (short)(a & 0xffff);
+        sf[s][j + 1] = (short)(a >> 16);
+        sf[2 + s][j] = (short)(c & 0xffff);
+        sf[2 + s][j + 1] = (short)(c >> 16);
+      }
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      if (dt > 0) kread(Kb, dt, ta);
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(ta[0]), "+v"(ta[1]), "+v"(ta[2]), "+v"(ta[3]), "+v"(ta[4]), "+v"(ta[5]), "+v"(ta[6]),
+                     "+v"(ta[7]));
+#pragma unroll
+      for (int ks4 = 0; ks4 < 4; ++ks4) dqacc[dt] = mfma32(cat44(ta[2 * ks4], ta[2 * ks4 + 1]), sf[ks4], dqacc[dt]);
+    }
+  };
+
+  const int nloop = ntiles + (STAGGER ? 1 : 0);
+  auto top = [&](int it) {
+    if (it < ntiles) {
+      if (it + 1 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (it + 2 < ntiles) issue(it + 2);
+  };
+  if (late) {
+    f32x16 s0, s1, p0, p1;
+    bool pending = false;
+    for (int it = 0; it < nloop; ++it) {
+      top(it);
+      if (pending) grad(it - 1, s0, s1, p0, p1);
+      pending = it < ntiles && (!causal || it * BN <= q0w + 31);
+      if (pending) scores(it, s0, s1, p0, p1);
+      asm volatile("" ::: "memory");
+    }
+  } else {
+    for (int it = 0; it < nloop; ++it) {
+      top(it);
+      if (it < ntiles && (!causal || it * BN <= q0w + 31)) {
+        f32x16 s0, s1, p0, p1;
+        scores(it, s0, s1, p0, p1);
+        grad(it, s0, s1, p0, p1);
+      }
+      asm volatile("" ::: "memory");
+    }
+  }
+#undef KBUF
+#undef VBUF
+  bf16_t* dp = dq + (int64_t)(b * S + qi) * dqs + hq * D;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      u32x2 w;
+      w[0] = pack2(dqacc[dt][4 * g4] * scale, dqacc[dt][4 * g4 + 1] * scale);
+      w[1] = pack2(dqacc[dt][4 * g4 + 2] * scale, dqacc[dt][4 * g4 + 3] * scale);
+      *reinterpret_cast<u32x2*>(dp + dt * 32 + 8 * g4 + 4 * hh) = w;
+    }
+  }
+}
+
 // dk/dv = bf16(sum over the GQA group of the per-q-head partials)
 template <int D>
 __global__ void __launch_bounds__(256) fa_bwd_finalize_kernel(const float* __restrict__ dk_part,
@@ -435,8 +614,31 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
   }
   fa_bwd_dkdv_kernel<D, NW><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(
       q, k, v, dout, lse, delta, dk_part, dv_part, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);
-  fa_bwd_dq_kernel<D, NW><<<B * Hq * (S / (32 * NW)), NW * 64, lds_q, stream>>>(
-      q, k, v, dout, lse, delta, dq, B, S, Hq, Hkv, qs, ks, vs, dos, dqs, scale, causal);
+  static const int dq_variant = [] {
+    const char* e = getenv("KOP_DQ_VARIANT");
+    return e ? atoi(e) : 9;
+  }();
+  if (S % 256 == 0 && dq_variant >= 8) {
+    const bool stg = dq_variant == 9;
+    const size_t lds8 = (stg ? 4 : 3) * 2 * 64 * (D * 2);
+    static bool attr8 = false;
+    if (!attr8) {
+      (void)hipFuncSetAttribute((const void*)fa_bwd_dq8_kernel<D, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(4 * 2 * 64 * (D * 2)));
+      (void)hipFuncSetAttribute((const void*)fa_bwd_dq8_kernel<D, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)(3 * 2 * 64 * (D * 2)));
+      attr8 = true;
+    }
+    if (stg)
+      fa_bwd_dq8_kernel<D, true><<<B * Hq * (S / 256), 512, lds8, stream>>>(q, k, v, dout, lse, delta, dq, B, S, Hq,
+                                                                            Hkv, qs, ks, vs, dos, dqs, scale, causal);
+    else
+      fa_bwd_dq8_kernel<D, false><<<B * Hq * (S / 256), 512, lds8, stream>>>(q, k, v, dout, lse, delta, dq, B, S, Hq,
+                                                                             Hkv, qs, ks, vs, dos, dqs, scale, causal);
+  } else {
+    fa_bwd_dq_kernel<D, NW><<<B * Hq * (S / (32 * NW)), NW * 64, lds_q, stream>>>(
+        q, k, v, dout, lse, delta, dq, B, S, Hq, Hkv, qs, ks, vs, dos, dqs, scale, causal);
+  }
   fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs);
 }
 

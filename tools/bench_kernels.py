@@ -15,7 +15,12 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+ITERS = [None]
+
+
 def timeit(fn, iters=20, warmup=3):
+    if ITERS[0] is not None:
+        iters, warmup = ITERS[0], 1
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
@@ -32,7 +37,7 @@ def emit(**kw):
     print(json.dumps(kw), flush=True)
 
 
-def bench_attn(B, S, Hq, Hkv, D, causal=True):
+def bench_attn(B, S, Hq, Hkv, D, causal=True, sdpa=True):
     from kubeoperator_amd.ops import load
 
     lib = load()
@@ -54,6 +59,8 @@ def bench_attn(B, S, Hq, Hkv, D, causal=True):
     emit(kernel="flash_attn_bwd", B=B, S=S, Hq=Hq, Hkv=Hkv, D=D, ms=round(t, 4),
          tflops=round(2.5 * flops_fwd / t / 1e9, 1))
     # reference point: torch SDPA (aotriton / CK inside PyTorch-ROCm)
+    if not sdpa:
+        return
     try:
         qh = q.reshape(B, S, Hq, D).transpose(1, 2).contiguous()
         kh = k.reshape(B, S, Hkv, D).transpose(1, 2).repeat_interleave(Hq // Hkv, 1).contiguous()
@@ -134,11 +141,14 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--seq", type=int, default=8192)
     ap.add_argument("--only", default="all")
+    ap.add_argument("--iters", type=int, default=None)
+    ap.add_argument("--no-sdpa", action="store_true")
     a = ap.parse_args()
+    ITERS[0] = a.iters
     emit(device=torch.cuda.get_device_name(0), arch=torch.cuda.get_device_properties(0).gcnArchName)
     if a.only in ("all", "attn"):
-        bench_attn(1, a.seq, 32, 8, 128)
-        bench_attn(4, 1024, 12, 12, 64)
+        bench_attn(1, a.seq, 32, 8, 128, sdpa=not a.no_sdpa)
+        bench_attn(4, 1024, 12, 12, 64, sdpa=not a.no_sdpa)
     if a.only in ("all", "mem"):
         bench_mem()
     if a.only in ("all", "gemm"):

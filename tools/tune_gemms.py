@@ -1,0 +1,84 @@
+"""Offline hipBLASLt solution tuning for the training step's GEMM shapes (TunableOp), one shape at a time
+with a progress line per shape (a long silent tuning run looks hung to the job runner).
+
+1. one training step with TunableOp recording (not tuning) every GEMM it calls;
+2. each recorded GEMM is tuned on its own (max KOP_TUNE_MS ms / KOP_TUNE_ITERS iterations per solution);
+3. the winners are written to kubeoperator_amd/tuning/tunableop_results_gfx950.csv, which bench.py and the
+   trainer load read-only (``--gemm-tuning use``).
+
+Usage (one MI355X): python tools/tune_gemms.py [--model llama3_8b --seq 8192 --mbs 1]
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3_8b")
+    ap.add_argument("--seq", type=int, default=8192)
+    ap.add_argument("--mbs", type=int, default=1)
+    a = ap.parse_args()
+
+    import torch
+    import torch.cuda.tunable as tun
+
+    from kubeoperator_amd.parallel.dist import init_distributed
+    from kubeoperator_amd.train import SyntheticTokens, TrainConfig, Trainer
+    from kubeoperator_amd.train.gemm_tuning import results_path
+
+    out = results_path()
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    untuned = os.path.join(os.path.dirname(out), "untuned_gemms.csv")
+    for p in (untuned,):
+        if os.path.exists(p):
+            os.remove(p)
+    os.environ["PYTORCH_TUNABLEOP_UNTUNED_FILENAME"] = untuned
+    tun.enable(True)
+    tun.tuning_enable(False)
+    tun.record_untuned_enable(True)
+    tun.set_filename(out, insert_device_ordinal=False)
+
+    info = init_distributed("auto")
+    tr = Trainer(TrainConfig(model=a.model, micro_batch=a.mbs, seq_len=a.seq, warmup_steps=10, total_steps=100), info)
+    data = SyntheticTokens(tr.cfg.vocab_size, a.mbs, a.seq, info.device, seed=1)
+    tr.train_step(data.batches(1))
+    torch.cuda.synchronize()
+    tun.record_untuned_enable(False)
+    # the untuned file is flushed when recording stops / at exit; give the writer a moment
+    for _ in range(50):
+        if os.path.exists(untuned) and os.path.getsize(untuned) > 0:
+            break
+        time.sleep(0.1)
+    cands = [p for p in (untuned, untuned.replace(".csv", "0.csv")) if os.path.exists(p)]
+    if not cands:
+        print("no untuned GEMM file was written", flush=True)
+        return 1
+    lines = [ln for ln in open(cands[0]) if ln.startswith(("Gemm", "ScaledGemm"))]
+    lines = sorted(set(lines), key=lines.index)
+    print(f"{len(lines)} distinct GEMMs to tune", flush=True)
+
+    tun.tuning_enable(True)
+    tun.set_max_tuning_duration(int(os.environ.get("KOP_TUNE_MS", "30")))
+    tun.set_max_tuning_iterations(int(os.environ.get("KOP_TUNE_ITERS", "10")))
+    dev = torch.cuda.current_device()
+    for i, ln in enumerate(lines):
+        t0 = time.time()
+        tun._process_single_offline_gemm(ln, dev)
+        torch.cuda.synchronize()
+        print(f"[{i + 1}/{len(lines)}] {time.time() - t0:6.1f}s {ln.strip()[:160]}", flush=True)
+        tun.write_file()
+    tun.write_file()
+    res = tun.get_results()
+    print(f"wrote {len(res)} tuned results to {out}", flush=True)
+    for r in res:
+        print("  ", r, flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,9 +1,22 @@
 // Shared device helpers of the flash-attention kernels (gfx950): MFMA wrapper, LDS row / transposed reads,
 // the swizzled LDS tile image, LDS-DMA issue and the XCD-aware block remap.
 #pragma once
+#include <type_traits>
+#include <utility>
+
 #include "common.h"
 
 namespace kop {
+// compile-time loop: f(std::integral_constant<int, i>{}) for i = 0 .. N-1 (indices usable as template args)
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
 
 __device__ __forceinline__ bf16x4 lds_tr_read(const char* p) {
@@ -20,8 +33,34 @@ __device__ __forceinline__ bf16x4 lds_tr_read_asm(const char* p) {
   return r;
 }
 __device__ __forceinline__ bf16x8 lds_read8(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
+// Transposed read at a lane base address (VGPR) + compile-time byte offset (the instruction's offset field).
+template <int OFF>
+__device__ __forceinline__ bf16x4 lds_tr_read_off(uint32_t base) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset field is 16 bits");
+  bf16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(base), "n"(OFF));
+  return r;
+}
+// Retire transposed reads: wait until at most CNT LDS ops are outstanding and tell hipcc the NR fragments
+// in t[] are written at that point (they come from inline-asm reads it cannot track).
+template <int NR, int CNT>
+__device__ __forceinline__ void wait_tr(bf16x4* t) {
+  static_assert(NR == 4 || NR == 8, "4 or 8 fragments");
+  if constexpr (NR == 8)
+    asm volatile("s_waitcnt lgkmcnt(%8)"
+                 : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]), "+v"(t[7])
+                 : "n"(CNT));
+  else
+    asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]) : "n"(CNT));
+}
 __device__ __forceinline__ bf16x8 cat44(bf16x4 a, bf16x4 b) {
   return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+}
+// accumulator registers 8h .. 8h+7 -> one bf16x8 MFMA operand (4 v_cvt_pk_bf16_f32, no sub-word moves)
+__device__ __forceinline__ bf16x8 pack_acc8(const f32x16& s, int h) {
+  const u32x4 w = {pack2(s[8 * h], s[8 * h + 1]), pack2(s[8 * h + 2], s[8 * h + 3]), pack2(s[8 * h + 4], s[8 * h + 5]),
+                   pack2(s[8 * h + 6], s[8 * h + 7])};
+  return __builtin_bit_cast(bf16x8, w);
 }
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -59,6 +98,29 @@ __device__ __forceinline__ void dma_tile(char* lds, const bf16_t* src, int64_t r
     const int piece = wid + i * NW;
     const int row = piece * RPP + prow;
     const int ch = pslot ^ swz_xor<ROWB>(row);
+    glds16(src + (int64_t)row * row_stride + ch * 8, lds + piece * 1024);
+  }
+}
+
+// Sub-tiled image (guide T10 image (a)): 8-row x 64-byte subtiles of 512 B, XOR-swizzled inside, so
+// ds_read_b128 row reads and ds_read_b64_tr_b16 transposed reads are both conflict-free AND every read of a
+// 32x32x16 operand is one of TWO lane base addresses plus a compile-time immediate (no per-read VALU).
+template <int ROWB>
+__device__ __forceinline__ int swza(int row, int ch) {
+  return (ROWB * 8) * (row >> 3) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
+}
+// LDS-DMA fill of a sub-tiled [ROWS][ROWB] image: 1-KiB pieces over NW waves; lane l of piece p lands at
+// byte 1024p + 16l, so its SOURCE (row, chunk) is the one the image puts there.
+template <int ROWB, int NW, int ROWS>
+__device__ __forceinline__ void dma_tile_a(char* lds, const bf16_t* src, int64_t row_stride, int wid, int lane) {
+  constexpr int PIECES = ROWS * ROWB / 1024, PPB = ROWB / 128;  // pieces per 8-row block
+  static_assert(PIECES % NW == 0, "tile pieces must split evenly over the waves");
+  const int lrow = (lane & 31) >> 2, lhi = lane >> 5, lslot = lane & 3;
+#pragma unroll
+  for (int i = 0; i < PIECES / NW; ++i) {
+    const int piece = wid + i * NW;
+    const int row = 8 * (piece / PPB) + lrow;
+    const int ch = 4 * (2 * (piece % PPB) + lhi) + (lslot ^ ((row >> 2) & 3));
     glds16(src + (int64_t)row * row_stride + ch * 8, lds + piece * 1024);
   }
 }

@@ -30,9 +30,13 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return *reinterpret_cast<bf16_t*>(&h);
 }
 
-// pack two floats into one dword of two bf16 (lo in bits 0..15)
+// pack two floats into one dword of two bf16 (lo in bits 0..15), round-to-nearest-even: a vector
+// conversion lowers to ONE v_cvt_pk_bf16_f32 (two scalar conversions + an OR would be three instructions)
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  const f32x2_t v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
 
 // 8 x bf16 <-> 8 x f32 for a 16-byte vector

@@ -172,19 +172,8 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
         sacc[j] = p;
         dpacc[j] = p * dpacc[j];
       }
-      bf16x8 pb[2], sb[2];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-#pragma unroll
-        for (int j = 0; j < 8; j += 2) {
-          const uint32_t a = pack2(sacc[8 * s + j], sacc[8 * s + j + 1]);
-          const uint32_t c = pack2(dpacc[8 * s + j], dpacc[8 * s + j + 1]);
-          pb[s][j] = (short)(a & 0xffff);
-          pb[s][j + 1] = (short)(a >> 16);
-          sb[s][j] = (short)(c & 0xffff);
-          sb[s][j + 1] = (short)(c >> 16);
-        }
-      }
+      const bf16x8 pb[2] = {pack_acc8(sacc, 0), pack_acc8(sacc, 1)};
+      const bf16x8 sb[2] = {pack_acc8(dpacc, 0), pack_acc8(dpacc, 1)};
 #pragma unroll
       for (int dt = 0; dt < D / 32; ++dt) {
         const int col = dt * 32 + 16 * tg1 + 4 * tp;
@@ -408,8 +397,8 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq8_kernel(
   const bf16_t* kbase = k + (int64_t)(b * S) * ks + kvh * D;
   const bf16_t* vbase = v + (int64_t)(b * S) * vs + kvh * D;
   auto issue = [&](int t) {
-    dma_tile<ROWB, NW, BN>(KBUF(t % NSLOT), kbase + (int64_t)(t * BN) * ks, ks, wid, lane);
-    dma_tile<ROWB, NW, BN>(VBUF(t % NSLOT), vbase + (int64_t)(t * BN) * vs, vs, wid, lane);
+    dma_tile_a<ROWB, NW, BN>(KBUF(t % NSLOT), kbase + (int64_t)(t * BN) * ks, ks, wid, lane);
+    dma_tile_a<ROWB, NW, BN>(VBUF(t % NSLOT), vbase + (int64_t)(t * BN) * vs, vs, wid, lane);
   };
   issue(0);
   if (ntiles > 1) issue(1);
@@ -436,6 +425,16 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq8_kernel(
   for (int i = 0; i < DT; ++i) dqacc[i] = f32x16{0};
   if (wid >= 4) __builtin_amdgcn_s_setprio(1);
 
+  // lane bases of the sub-tiled image (swza), as in fa_fwd8_kernel: rows r / r+32 at chunk 2kk+hh, and
+  // the transposed reads of rows R0 + 4hh + tq
+  constexpr int RB = ROWB * 8;
+  const int rb_lane0 = RB * (r >> 3) + 64 * (r & 7) + 16 * (hh ^ ((r >> 2) & 3));
+  const int rb_lane1 = RB * (r >> 3) + 64 * (r & 7) + 16 * ((2 + hh) ^ ((r >> 2) & 3));
+  const int tb_lane0 = 64 * (4 * hh + tq) + 16 * ((2 * tg1 + (tp >> 1)) ^ hh) + 8 * (tp & 1);
+  const int tb_lane1 = 64 * (4 * hh + tq) + 16 * ((2 * tg1 + (tp >> 1)) ^ (2 + hh)) + 8 * (tp & 1);
+  auto raddr = [&](const char* base, int kk, int half) {
+    return base + ((kk & 1) ? rb_lane1 : rb_lane0) + RB * 4 * half + 512 * (kk >> 1);
+  };
   // S^T = K.Q^T and dP^T = V.dO^T for the 64 keys of tile t
   auto scores = [&](int t, f32x16& s0, f32x16& s1, f32x16& p0, f32x16& p1) {
     const char* Kb = KBUF(t % NSLOT);
@@ -443,31 +442,33 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq8_kernel(
     s0 = s1 = p0 = p1 = f32x16{0};
 #pragma unroll
     for (int kk = 0; kk < D / 16; ++kk) {
-      const bf16x8 ka = lds_read8(Kb + swz<ROWB>(r, 2 * kk + hh));
-      const bf16x8 kb = lds_read8(Kb + swz<ROWB>(32 + r, 2 * kk + hh));
-      const bf16x8 va = lds_read8(Vb + swz<ROWB>(r, 2 * kk + hh));
-      const bf16x8 vb = lds_read8(Vb + swz<ROWB>(32 + r, 2 * kk + hh));
+      const bf16x8 ka = lds_read8(raddr(Kb, kk, 0));
+      const bf16x8 kb = lds_read8(raddr(Kb, kk, 1));
+      const bf16x8 va = lds_read8(raddr(Vb, kk, 0));
+      const bf16x8 vb = lds_read8(raddr(Vb, kk, 1));
       s0 = mfma32(ka, qf[kk], s0);
       s1 = mfma32(kb, qf[kk], s1);
       p0 = mfma32(va, of[kk], p0);
       p1 = mfma32(vb, of[kk], p1);
     }
   };
-  auto kread = [&](const char* Kb, int dt, bf16x4* t) {
-    const int col = dt * 32 + 16 * tg1 + 4 * tp;
-    const int ch = col >> 3, bo = (col & 7) * 2;
-#pragma unroll
-    for (int ks4 = 0; ks4 < 4; ++ks4) {
-      const int rowA = (ks4 >> 1) * 32 + 16 * (ks4 & 1) + 4 * hh + tq;
-      t[2 * ks4] = lds_tr_read_asm(Kb + swz<ROWB>(rowA, ch) + bo);
-      t[2 * ks4 + 1] = lds_tr_read_asm(Kb + swz<ROWB>(rowA + 8, ch) + bo);
-    }
+  // K^T fragments of key group ks4 for every output block dt (independent dQ accumulators per MFMA)
+  constexpr int NR = 2 * DT;
+  auto kread = [&](const char* Kb, auto ks4c, bf16x4* t) {
+    constexpr int ks4 = decltype(ks4c)::value;
+    constexpr int R0 = (ks4 >> 1) * 32 + 16 * (ks4 & 1);
+    const uint32_t b0 = lds_addr(Kb) + tb_lane0, b1 = lds_addr(Kb) + tb_lane1;
+    static_for<DT>([&](auto dtc) {
+      constexpr int dt = decltype(dtc)::value;
+      t[2 * dt] = lds_tr_read_off<RB * (R0 >> 3) + 512 * dt>(((R0 >> 3) & 1) ? b1 : b0);
+      t[2 * dt + 1] = lds_tr_read_off<RB * ((R0 + 8) >> 3) + 512 * dt>((((R0 + 8) >> 3) & 1) ? b1 : b0);
+    });
   };
   // dS^T = P^T (dP^T - delta) and dQ^T += K^T . dS^T
   auto grad = [&](int t, f32x16& s0, f32x16& s1, f32x16& p0, f32x16& p1) {
     const char* Kb = KBUF(t % NSLOT);
-    bf16x4 ta[8];
-    kread(Kb, 0, ta);  // flies under the dS VALU work
+    bf16x4 ta[NR];
+    kread(Kb, std::integral_constant<int, 0>{}, ta);  // flies under the dS VALU work
     const int kv0 = t * BN;
     const bool diag = causal && kv0 + BN - 1 > q0w;
 #pragma unroll
@@ -480,28 +481,14 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq8_kernel(
       s0[j] = pa * (p0[j] - dl);
       s1[j] = pb * (p1[j] - dl);
     }
-    bf16x8 sf[4];
+    const bf16x8 sf[4] = {pack_acc8(s0, 0), pack_acc8(s0, 1), pack_acc8(s1, 0), pack_acc8(s1, 1)};
+    static_for<4>([&](auto ks4c) {
+      constexpr int ks4 = decltype(ks4c)::value;
+      if constexpr (ks4 > 0) kread(Kb, ks4c, ta);
+      wait_tr<NR, 0>(ta);
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-#pragma unroll
-      for (int j = 0; j < 8; j += 2) {
-        const uint32_t a = pack2(s0[8 * s + j], s0[8 * s + j + 1]);
-        const uint32_t c = pack2(s1[8 * s + j], s1[8 * s + j + 1]);
-        sf[s][j] = (short)(a & 0xffff);
-        sf[s][j + 1] = (short)(a >> 16);
-        sf[2 + s][j] = (short)(c & 0xffff);
-        sf[2 + s][j + 1] = (short)(c >> 16);
-      }
-    }
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      if (dt > 0) kread(Kb, dt, ta);
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(ta[0]), "+v"(ta[1]), "+v"(ta[2]), "+v"(ta[3]), "+v"(ta[4]), "+v"(ta[5]), "+v"(ta[6]),
-                     "+v"(ta[7]));
-#pragma unroll
-      for (int ks4 = 0; ks4 < 4; ++ks4) dqacc[dt] = mfma32(cat44(ta[2 * ks4], ta[2 * ks4 + 1]), sf[ks4], dqacc[dt]);
-    }
+      for (int dt = 0; dt < DT; ++dt) dqacc[dt] = mfma32(cat44(ta[2 * dt], ta[2 * dt + 1]), sf[ks4], dqacc[dt]);
+    });
   };
 
   const int nloop = ntiles + (STAGGER ? 1 : 0);

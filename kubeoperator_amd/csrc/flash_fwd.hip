@@ -249,17 +249,12 @@ __global__ void __launch_bounds__(512, 1) fa_fwd8_kernel(const bf16_t* __restric
 
   const bf16_t* kbase = k + (int64_t)(b * S) * ks + kvh * D;
   const bf16_t* vbase = v + (int64_t)(b * S) * vs + kvh * D;
-  const int prow = lane / SLOTS, pslot = lane % SLOTS;
+  (void)SLOTS;
+  (void)RPP;
   auto issue = [&](int t) {
     const int sl = t % NSLOT;
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const int piece = wid * PPW + i;
-      const int row = piece * RPP + prow;
-      const int ch = pslot ^ swz_xor<ROWB>(row);
-      glds16(kbase + (int64_t)(t * BN + row) * ks + ch * 8, KBUF(sl) + piece * 1024);
-      glds16(vbase + (int64_t)(t * BN + row) * vs + ch * 8, VBUF(sl) + piece * 1024);
-    }
+    dma_tile_a<ROWB, NW, BN>(KBUF(sl), kbase + (int64_t)(t * BN) * ks, ks, wid, lane);
+    dma_tile_a<ROWB, NW, BN>(VBUF(sl), vbase + (int64_t)(t * BN) * vs, vs, wid, lane);
   };
   issue(0);
   if (ntiles > 1) issue(1);
@@ -280,18 +275,29 @@ __global__ void __launch_bounds__(512, 1) fa_fwd8_kernel(const bf16_t* __restric
   if (wid >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the second-dispatched half (T5)
 
   // S^T = K . Q^T for the 64 keys of tile t (two 32-key accumulators), causal mask applied
+  // lane base offsets of the sub-tiled image (swza): K rows r / r+32 at chunk 2kk+hh are
+  // kb_lane[kk&1] + RB*4*(row>=32) + 512*(kk>>1); V^T tr-reads of rows R0 + 4hh + tq (R0 % 8 == 0) at
+  // column block dt are vb_lane[(R0>>3)&1] + RB*(R0>>3) + 512*dt (RB = 8 rows of the image)
+  constexpr int RB = ROWB * 8;
+  const int kb_lane0 = RB * (r >> 3) + 64 * (r & 7) + 16 * (hh ^ ((r >> 2) & 3));
+  const int kb_lane1 = RB * (r >> 3) + 64 * (r & 7) + 16 * ((2 + hh) ^ ((r >> 2) & 3));
+  const int vb_lane0 = 64 * (4 * hh + tq) + 16 * ((2 * tg1 + (tp >> 1)) ^ hh) + 8 * (tp & 1);
+  const int vb_lane1 = 64 * (4 * hh + tq) + 16 * ((2 * tg1 + (tp >> 1)) ^ (2 + hh)) + 8 * (tp & 1);
+  auto kaddr = [&](const char* Kb, int kk, int half) {
+    return Kb + ((kk & 1) ? kb_lane1 : kb_lane0) + RB * 4 * half + 512 * (kk >> 1);
+  };
   auto qk = [&](int t, f32x16& s0, f32x16& s1) {
     const char* Kb = KBUF(t % NSLOT);
     s0 = f32x16{0};
     s1 = f32x16{0};
-    bf16x8 ka = lds_read8(Kb + swz<ROWB>(r, hh));
-    bf16x8 kb = lds_read8(Kb + swz<ROWB>(32 + r, hh));
+    bf16x8 ka = lds_read8(kaddr(Kb, 0, 0));
+    bf16x8 kb = lds_read8(kaddr(Kb, 0, 1));
 #pragma unroll
     for (int kk = 0; kk < D / 16; ++kk) {
       bf16x8 na, nb;
       if (kk + 1 < D / 16) {
-        na = lds_read8(Kb + swz<ROWB>(r, 2 * (kk + 1) + hh));
-        nb = lds_read8(Kb + swz<ROWB>(32 + r, 2 * (kk + 1) + hh));
+        na = lds_read8(kaddr(Kb, kk + 1, 0));
+        nb = lds_read8(kaddr(Kb, kk + 1, 1));
       }
       s0 = mfma32(ka, qf[kk], s0);
       s1 = mfma32(kb, qf[kk], s1);
@@ -311,23 +317,25 @@ __global__ void __launch_bounds__(512, 1) fa_fwd8_kernel(const bf16_t* __restric
       }
     }
   };
-  // V^T fragments of output block dt (8 transposed reads, retired by the caller's counted wait)
-  auto vread = [&](const char* Vb, int dt, bf16x4* t) {
-    const int col = dt * 32 + 16 * tg1 + 4 * tp;
-    const int ch = col >> 3, bo = (col & 7) * 2;
-#pragma unroll
-    for (int ks4 = 0; ks4 < 4; ++ks4) {
-      const int rowA = (ks4 >> 1) * 32 + 16 * (ks4 & 1) + 4 * hh + tq;
-      t[2 * ks4] = lds_tr_read_asm(Vb + swz<ROWB>(rowA, ch) + bo);
-      t[2 * ks4 + 1] = lds_tr_read_asm(Vb + swz<ROWB>(rowA + 8, ch) + bo);
-    }
+  // V^T fragments of key group ks4 (16 keys) for every 32-column output block dt (NR = 2*DT transposed
+  // reads, each a lane base + immediate); consecutive P.V MFMAs go to DT independent accumulators
+  constexpr int NR = 2 * DT;
+  auto vread = [&](const char* Vb, auto ks4c, bf16x4* t) {
+    constexpr int ks4 = decltype(ks4c)::value;
+    constexpr int R0 = (ks4 >> 1) * 32 + 16 * (ks4 & 1);  // rows R0 + 4hh + tq and R0 + 8 + ...
+    const uint32_t b0 = lds_addr(Vb) + vb_lane0, b1 = lds_addr(Vb) + vb_lane1;
+    static_for<DT>([&](auto dtc) {
+      constexpr int dt = decltype(dtc)::value;
+      t[2 * dt] = lds_tr_read_off<RB * (R0 >> 3) + 512 * dt>(((R0 >> 3) & 1) ? b1 : b0);
+      t[2 * dt + 1] = lds_tr_read_off<RB * ((R0 + 8) >> 3) + 512 * dt>((((R0 + 8) >> 3) & 1) ? b1 : b0);
+    });
   };
   // online softmax of tile t's scores and O^T += V^T . P^T
   auto softmax_pv = [&](int t, f32x16& s0, f32x16& s1, auto db_tag) {
     constexpr bool DB = decltype(db_tag)::value;  // double-buffered V^T reads (needs 16 more VGPRs)
     const char* Vb = VBUF(t % NSLOT);
-    bf16x4 ta[8], tb[DB ? 8 : 1];
-    vread(Vb, 0, ta);  // flies under the softmax
+    bf16x4 ta[NR], tb[DB ? NR : 1];
+    vread(Vb, std::integral_constant<int, 0>{}, ta);  // flies under the softmax
     float mx = fmaxf(s0[0], s1[0]);
 #pragma unroll
     for (int j = 1; j < 16; ++j) mx = fmaxf(mx, fmaxf(s0[j], s1[j]));
@@ -349,41 +357,23 @@ __global__ void __launch_bounds__(512, 1) fa_fwd8_kernel(const bf16_t* __restric
       ls += s0[j] + s1[j];
     }
     l += ls;
-    bf16x8 pf[4];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-#pragma unroll
-      for (int j = 0; j < 8; j += 2) {
-        const uint32_t a = pack2(s0[8 * s + j], s0[8 * s + j + 1]);
-        const uint32_t c = pack2(s1[8 * s + j], s1[8 * s + j + 1]);
-        pf[s][j] = (short)(a & 0xffff);
-        pf[s][j + 1] = (short)(a >> 16);
-        pf[2 + s][j] = (short)(c & 0xffff);
-        pf[2 + s][j + 1] = (short)(c >> 16);
-      }
-    }
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      bf16x4* cur = (DB && (dt & 1)) ? tb : ta;
-      bf16x4* nxt = (DB && (dt & 1)) ? ta : tb;
-      if (!DB) {
-        if (dt > 0) vread(Vb, dt, cur);
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]), "+v"(cur[4]), "+v"(cur[5]),
-                       "+v"(cur[6]), "+v"(cur[7]));
-      } else if (dt + 1 < DT) {
-        vread(Vb, dt + 1, nxt);
-        asm volatile("s_waitcnt lgkmcnt(8)"
-                     : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]), "+v"(cur[4]), "+v"(cur[5]),
-                       "+v"(cur[6]), "+v"(cur[7]));
+    const bf16x8 pf[4] = {pack_acc8(s0, 0), pack_acc8(s0, 1), pack_acc8(s1, 0), pack_acc8(s1, 1)};
+    static_for<4>([&](auto ks4c) {
+      constexpr int ks4 = decltype(ks4c)::value;
+      bf16x4* cur = (DB && (ks4 & 1)) ? tb : ta;
+      bf16x4* nxt = (DB && (ks4 & 1)) ? ta : tb;
+      if constexpr (!DB) {
+        if constexpr (ks4 > 0) vread(Vb, ks4c, cur);
+        wait_tr<NR, 0>(cur);
+      } else if constexpr (ks4 + 1 < 4) {
+        vread(Vb, std::integral_constant<int, ks4 + 1>{}, nxt);
+        wait_tr<NR, NR>(cur);
       } else {
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]), "+v"(cur[4]), "+v"(cur[5]),
-                       "+v"(cur[6]), "+v"(cur[7]));
+        wait_tr<NR, 0>(cur);
       }
 #pragma unroll
-      for (int ks4 = 0; ks4 < 4; ++ks4) oacc[dt] = mfma32(cat44(cur[2 * ks4], cur[2 * ks4 + 1]), pf[ks4], oacc[dt]);
-    }
+      for (int dt = 0; dt < DT; ++dt) oacc[dt] = mfma32(cat44(cur[2 * dt], cur[2 * dt + 1]), pf[ks4], oacc[dt]);
+    });
   };
 
   const int nloop = ntiles + (STAGGER ? 1 : 0);

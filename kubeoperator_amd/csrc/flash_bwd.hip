@@ -101,8 +101,8 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
   auto issue = [&](int qt, int stage) {
     char* base = smem + KB + stage * STAGE;
     const int q0 = qt * BQ;
-    dma_tile<ROWB, NW, BQ>(base, qbase + (int64_t)q0 * qs, qs, wid, lane);
-    dma_tile<ROWB, NW, BQ>(base + QT, dobase + (int64_t)q0 * dos, dos, wid, lane);
+    dma_tile_a<ROWB, NW, BQ>(base, qbase + (int64_t)q0 * qs, qs, wid, lane);
+    dma_tile_a<ROWB, NW, BQ>(base + QT, dobase + (int64_t)q0 * dos, dos, wid, lane);
     if (wid == 0) {
       // lanes 0-7: lse[q0..q0+31], lanes 8-15: delta[...]; lanes 16-63 repeat into the unused tail
       const int l = lane & 15;
@@ -112,8 +112,18 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
   };
 
   // K block of the workgroup -> LDS (counted with the first stage)
-  dma_tile<ROWB, NW, BN>(Kl, k + (int64_t)(b * S + k0) * ks + kvh * D, ks, wid, lane);
+  dma_tile_a<ROWB, NW, BN>(Kl, k + (int64_t)(b * S + k0) * ks + kvh * D, ks, wid, lane);
   issue(qt0, 0);
+  // lane bases of the sub-tiled images (swza): row reads of rows r (+32*i) at chunk 2kk+hh, transposed
+  // reads of rows R0 + 4hh + tq
+  constexpr int RB = ROWB * 8;
+  const int rb_lane0 = RB * (r >> 3) + 64 * (r & 7) + 16 * (hh ^ ((r >> 2) & 3));
+  const int rb_lane1 = RB * (r >> 3) + 64 * (r & 7) + 16 * ((2 + hh) ^ ((r >> 2) & 3));
+  const int tb_lane0 = 64 * (4 * hh + tq) + 16 * ((2 * tg1 + (tp >> 1)) ^ hh) + 8 * (tp & 1);
+  const int tb_lane1 = 64 * (4 * hh + tq) + 16 * ((2 * tg1 + (tp >> 1)) ^ (2 + hh)) + 8 * (tp & 1);
+  auto raddr = [&](const char* base, int kk) {
+    return base + ((kk & 1) ? rb_lane1 : rb_lane0) + 512 * (kk >> 1);
+  };
   // V^T operand fragments of this wave's 32 keys (B operand of dP = dO.V^T; key = k0w + r), resident
   bf16x8 vf[D / 16];
   {
@@ -157,9 +167,9 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
       }
 #pragma unroll
       for (int kk = 0; kk < D / 16; ++kk) {
-        const bf16x8 qa = lds_read8(Ql + swz<ROWB>(r, 2 * kk + hh));
-        const bf16x8 kbf = lds_read8(Kl + swz<ROWB>(32 * wid + r, 2 * kk + hh));
-        const bf16x8 oa = lds_read8(Ol + swz<ROWB>(r, 2 * kk + hh));
+        const bf16x8 qa = lds_read8(raddr(Ql, kk) );
+        const bf16x8 kbf = lds_read8(raddr(Kl, kk) + RB * 4 * wid);
+        const bf16x8 oa = lds_read8(raddr(Ol, kk));
         sacc = mfma32(qa, kbf, sacc);
         dpacc = mfma32(oa, vf[kk], dpacc);
       }
@@ -174,28 +184,27 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
       }
       const bf16x8 pb[2] = {pack_acc8(sacc, 0), pack_acc8(sacc, 1)};
       const bf16x8 sb[2] = {pack_acc8(dpacc, 0), pack_acc8(dpacc, 1)};
-#pragma unroll
-      for (int dt = 0; dt < D / 32; ++dt) {
-        const int col = dt * 32 + 16 * tg1 + 4 * tp;
-        const int ch = col >> 3, bo = (col & 7) * 2;
+      // transposed dO / Q reads: rows 16s + 4hh + tq (+8) are tb_lane[(row0>>3)&1] + RB*(row0>>3), column
+      // block dt is +512*dt (sub-tiled image, all immediates)
+      const uint32_t o0 = lds_addr(Ol) + tb_lane0, o1 = lds_addr(Ol) + tb_lane1;
+      const uint32_t q0a = lds_addr(Ql) + tb_lane0, q1a = lds_addr(Ql) + tb_lane1;
+      static_for<D / 32>([&](auto dtc) {
+        constexpr int dt = decltype(dtc)::value;
         bf16x4 t[8];
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const int rowA = 16 * s + 4 * hh + tq;
-          t[4 * s + 0] = lds_tr_read_asm(Ol + swz<ROWB>(rowA, ch) + bo);
-          t[4 * s + 1] = lds_tr_read_asm(Ol + swz<ROWB>(rowA + 8, ch) + bo);
-          t[4 * s + 2] = lds_tr_read_asm(Ql + swz<ROWB>(rowA, ch) + bo);
-          t[4 * s + 3] = lds_tr_read_asm(Ql + swz<ROWB>(rowA + 8, ch) + bo);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]),
-                       "+v"(t[7]));
+        static_for<2>([&](auto sc) {
+          constexpr int s = decltype(sc)::value;
+          t[4 * s + 0] = lds_tr_read_off<RB * 2 * s + 512 * dt>(o0);
+          t[4 * s + 1] = lds_tr_read_off<RB * (2 * s + 1) + 512 * dt>(o1);
+          t[4 * s + 2] = lds_tr_read_off<RB * 2 * s + 512 * dt>(q0a);
+          t[4 * s + 3] = lds_tr_read_off<RB * (2 * s + 1) + 512 * dt>(q1a);
+        });
+        wait_tr<8, 0>(t);
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           dvacc[dt] = mfma32(cat44(t[4 * s], t[4 * s + 1]), pb[s], dvacc[dt]);
           dkacc[dt] = mfma32(cat44(t[4 * s + 2], t[4 * s + 3]), sb[s], dkacc[dt]);
         }
-      }
+      });
     }
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();  // stage is refilled by the next iteration's DMA

@@ -41,6 +41,23 @@ __device__ __forceinline__ bf16x4 lds_tr_read_off(uint32_t base) {
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(base), "n"(OFF));
   return r;
 }
+// Row read (ds_read_b128) at a lane base + immediate, hidden from hipcc's scheduler like the transposed
+// reads: hipcc would otherwise fold a prefetch chain into one register quad and wait on every read.
+template <int OFF>
+__device__ __forceinline__ bf16x8 lds_read8_off(uint32_t base) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset field is 16 bits");
+  bf16x8 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(base), "n"(OFF));
+  return r;
+}
+template <int CNT>
+__device__ __forceinline__ void wait_rows4(bf16x8* t) {
+  asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]) : "n"(CNT));
+}
+template <int CNT>
+__device__ __forceinline__ void wait_rows3(bf16x8* t) {
+  asm volatile("s_waitcnt lgkmcnt(%3)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]) : "n"(CNT));
+}
 // Retire transposed reads: wait until at most CNT LDS ops are outstanding and tell hipcc the NR fragments
 // in t[] are written at that point (they come from inline-asm reads it cannot track).
 template <int NR, int CNT>

@@ -165,13 +165,31 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
           dpacc[4 * g4 + e] = -dv[e];
         }
       }
-#pragma unroll
-      for (int kk = 0; kk < D / 16; ++kk) {
-        const bf16x8 qa = lds_read8(raddr(Ql, kk) );
-        const bf16x8 kbf = lds_read8(raddr(Kl, kk) + RB * 4 * wid);
-        const bf16x8 oa = lds_read8(raddr(Ol, kk));
-        sacc = mfma32(qa, kbf, sacc);
-        dpacc = mfma32(oa, vf[kk], dpacc);
+      (void)raddr;
+      {
+        // per k-step one group of 3 row reads (Q row r, K row 32*wid + r, dO row r), two in flight
+        const uint32_t qb0 = lds_addr(Ql) + rb_lane0, qb1 = lds_addr(Ql) + rb_lane1;
+        const uint32_t ob0 = lds_addr(Ol) + rb_lane0, ob1 = lds_addr(Ol) + rb_lane1;
+        const uint32_t kw0 = lds_addr(Kl) + rb_lane0 + RB * 4 * wid, kw1 = lds_addr(Kl) + rb_lane1 + RB * 4 * wid;
+        auto grp = [&](auto kc, bf16x8* dst) {
+          constexpr int kk = decltype(kc)::value;
+          dst[0] = lds_read8_off<512 * (kk >> 1)>((kk & 1) ? qb1 : qb0);
+          dst[1] = lds_read8_off<512 * (kk >> 1)>((kk & 1) ? kw1 : kw0);
+          dst[2] = lds_read8_off<512 * (kk >> 1)>((kk & 1) ? ob1 : ob0);
+        };
+        constexpr int NK = D / 16;
+        bf16x8 ga[3], gb[3];
+        grp(std::integral_constant<int, 0>{}, ga);
+        grp(std::integral_constant<int, 1>{}, gb);
+        static_for<NK>([&](auto kc) {
+          constexpr int kk = decltype(kc)::value;
+          bf16x8* cur = (kk & 1) ? gb : ga;
+          if constexpr (kk + 1 < NK) wait_rows3<3>(cur);
+          else wait_rows3<0>(cur);
+          sacc = mfma32(cur[0], cur[1], sacc);
+          dpacc = mfma32(cur[2], vf[kk], dpacc);
+          if constexpr (kk + 2 < NK) grp(std::integral_constant<int, kk + 2>{}, cur);
+        });
       }
       const int key = k0w + r;
 #pragma unroll
@@ -449,17 +467,32 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq8_kernel(
     const char* Kb = KBUF(t % NSLOT);
     const char* Vb = VBUF(t % NSLOT);
     s0 = s1 = p0 = p1 = f32x16{0};
-#pragma unroll
-    for (int kk = 0; kk < D / 16; ++kk) {
-      const bf16x8 ka = lds_read8(raddr(Kb, kk, 0));
-      const bf16x8 kb = lds_read8(raddr(Kb, kk, 1));
-      const bf16x8 va = lds_read8(raddr(Vb, kk, 0));
-      const bf16x8 vb = lds_read8(raddr(Vb, kk, 1));
-      s0 = mfma32(ka, qf[kk], s0);
-      s1 = mfma32(kb, qf[kk], s1);
-      p0 = mfma32(va, of[kk], p0);
-      p1 = mfma32(vb, of[kk], p1);
-    }
+    (void)raddr;
+    // per k-step one group of 4 row reads (K rows r, r+32; V rows r, r+32), two groups in flight
+    const uint32_t kb0 = lds_addr(Kb) + rb_lane0, kb1 = lds_addr(Kb) + rb_lane1;
+    const uint32_t vb0 = lds_addr(Vb) + rb_lane0, vb1 = lds_addr(Vb) + rb_lane1;
+    auto grp = [&](auto kc, bf16x8* dst) {
+      constexpr int kk = decltype(kc)::value;
+      dst[0] = lds_read8_off<512 * (kk >> 1)>((kk & 1) ? kb1 : kb0);
+      dst[1] = lds_read8_off<RB * 4 + 512 * (kk >> 1)>((kk & 1) ? kb1 : kb0);
+      dst[2] = lds_read8_off<512 * (kk >> 1)>((kk & 1) ? vb1 : vb0);
+      dst[3] = lds_read8_off<RB * 4 + 512 * (kk >> 1)>((kk & 1) ? vb1 : vb0);
+    };
+    constexpr int NK = D / 16;
+    bf16x8 ga[4], gb[4];
+    grp(std::integral_constant<int, 0>{}, ga);
+    grp(std::integral_constant<int, 1>{}, gb);
+    static_for<NK>([&](auto kc) {
+      constexpr int kk = decltype(kc)::value;
+      bf16x8* cur = (kk & 1) ? gb : ga;
+      if constexpr (kk + 1 < NK) wait_rows4<4>(cur);
+      else wait_rows4<0>(cur);
+      s0 = mfma32(cur[0], qf[kk], s0);
+      s1 = mfma32(cur[1], qf[kk], s1);
+      p0 = mfma32(cur[2], of[kk], p0);
+      p1 = mfma32(cur[3], of[kk], p1);
+      if constexpr (kk + 2 < NK) grp(std::integral_constant<int, kk + 2>{}, cur);
+    });
   };
   // K^T fragments of key group ks4 for every output block dt (independent dQ accumulators per MFMA)
   constexpr int NR = 2 * DT;

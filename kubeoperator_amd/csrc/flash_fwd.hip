@@ -286,26 +286,37 @@ __global__ void __launch_bounds__(512, 1) fa_fwd8_kernel(const bf16_t* __restric
   auto kaddr = [&](const char* Kb, int kk, int half) {
     return Kb + ((kk & 1) ? kb_lane1 : kb_lane0) + RB * 4 * half + 512 * (kk >> 1);
   };
+  (void)kaddr;
+  // K row fragments in groups of 4 reads (k-steps 2g, 2g+1 x rows r, r+32), two groups in flight, each
+  // retired by a counted lgkmcnt right before its MFMAs
+  constexpr int NG = D / 32;
+  auto kgroup = [&](uint32_t k0, uint32_t k1, auto gc, bf16x8* dst) {
+    constexpr int g = decltype(gc)::value;
+    static_for<2>([&](auto jc) {
+      constexpr int kk = 2 * g + decltype(jc)::value;
+      dst[2 * decltype(jc)::value] = lds_read8_off<512 * (kk >> 1)>((kk & 1) ? k1 : k0);
+      dst[2 * decltype(jc)::value + 1] = lds_read8_off<RB * 4 + 512 * (kk >> 1)>((kk & 1) ? k1 : k0);
+    });
+  };
   auto qk = [&](int t, f32x16& s0, f32x16& s1) {
     const char* Kb = KBUF(t % NSLOT);
+    const uint32_t k0 = lds_addr(Kb) + kb_lane0, k1 = lds_addr(Kb) + kb_lane1;
     s0 = f32x16{0};
     s1 = f32x16{0};
-    bf16x8 ka = lds_read8(kaddr(Kb, 0, 0));
-    bf16x8 kb = lds_read8(kaddr(Kb, 0, 1));
-#pragma unroll
-    for (int kk = 0; kk < D / 16; ++kk) {
-      bf16x8 na, nb;
-      if (kk + 1 < D / 16) {
-        na = lds_read8(kaddr(Kb, kk + 1, 0));
-        nb = lds_read8(kaddr(Kb, kk + 1, 1));
-      }
-      s0 = mfma32(ka, qf[kk], s0);
-      s1 = mfma32(kb, qf[kk], s1);
-      if (kk + 1 < D / 16) {
-        ka = na;
-        kb = nb;
-      }
-    }
+    bf16x8 ga[4], gb[4];
+    kgroup(k0, k1, std::integral_constant<int, 0>{}, ga);
+    if constexpr (NG > 1) kgroup(k0, k1, std::integral_constant<int, 1>{}, gb);
+    static_for<NG>([&](auto gc) {
+      constexpr int g = decltype(gc)::value;
+      bf16x8* cur = (g & 1) ? gb : ga;
+      if constexpr (g + 1 < NG) wait_rows4<4>(cur);
+      else wait_rows4<0>(cur);
+      s0 = mfma32(cur[0], qf[2 * g], s0);
+      s1 = mfma32(cur[1], qf[2 * g], s1);
+      s0 = mfma32(cur[2], qf[2 * g + 1], s0);
+      s1 = mfma32(cur[3], qf[2 * g + 1], s1);
+      if constexpr (g + 2 < NG) kgroup(k0, k1, std::integral_constant<int, g + 2>{}, cur);
+    });
     const int kv0 = t * BN;
     if (causal && kv0 + BN - 1 > q0w) {
       const int qi = q0w + r;

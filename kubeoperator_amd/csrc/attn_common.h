@@ -73,6 +73,31 @@ __device__ __forceinline__ void wait_tr(bf16x4* t) {
 __device__ __forceinline__ bf16x8 cat44(bf16x4 a, bf16x4 b) {
   return bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
+// v_max3_f32 without hipcc's canonicalising v_max on each MFMA result (fmaxf would emit 3 instructions)
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  float d;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+// max over the 32 scores of two accumulators: 16 v_max3
+__device__ __forceinline__ float max32(const f32x16& a, const f32x16& b) {
+  float m = max3f(a[0], b[0], a[1]);
+#pragma unroll
+  for (int j = 1; j < 16; ++j) m = max3f(m, a[j], b[j]);
+  return m;
+}
+// sum of the 32 values of two accumulators with packed adds (v_pk_add_f32: two lanes' worth per issue)
+__device__ __forceinline__ float sum32(const f32x16& a, const f32x16& b) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  f2 acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = f2{a[2 * i], a[2 * i + 1]} + f2{b[2 * i], b[2 * i + 1]};
+#pragma unroll
+  for (int i = 4; i < 8; ++i)
+    acc[i & 3] += f2{a[2 * i], a[2 * i + 1]} + f2{b[2 * i], b[2 * i + 1]};
+  const f2 s = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  return s[0] + s[1];
+}
 // accumulator registers 8h .. 8h+7 -> one bf16x8 MFMA operand (4 v_cvt_pk_bf16_f32, no sub-word moves)
 __device__ __forceinline__ bf16x8 pack_acc8(const f32x16& s, int h) {
   const u32x4 w = {pack2(s[8 * h], s[8 * h + 1]), pack2(s[8 * h + 2], s[8 * h + 3]), pack2(s[8 * h + 4], s[8 * h + 5]),

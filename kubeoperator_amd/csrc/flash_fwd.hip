@@ -347,9 +347,7 @@ __global__ void __launch_bounds__(512, 1) fa_fwd8_kernel(const bf16_t* __restric
     const char* Vb = VBUF(t % NSLOT);
     bf16x4 ta[NR], tb[DB ? NR : 1];
     vread(Vb, std::integral_constant<int, 0>{}, ta);  // flies under the softmax
-    float mx = fmaxf(s0[0], s1[0]);
-#pragma unroll
-    for (int j = 1; j < 16; ++j) mx = fmaxf(mx, fmaxf(s0[j], s1[j]));
+    float mx = max32(s0, s1);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mt = mx * scale_log2;
     if (__any(mt > m + 8.f)) {
@@ -360,14 +358,12 @@ __global__ void __launch_bounds__(512, 1) fa_fwd8_kernel(const bf16_t* __restric
 #pragma unroll
       for (int i = 0; i < DT; ++i) oacc[i] *= alpha;
     }
-    float ls = 0.f;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       s0[j] = __builtin_amdgcn_exp2f(fmaf(s0[j], scale_log2, -m));
       s1[j] = __builtin_amdgcn_exp2f(fmaf(s1[j], scale_log2, -m));
-      ls += s0[j] + s1[j];
     }
-    l += ls;
+    l += sum32(s0, s1);
     const bf16x8 pf[4] = {pack_acc8(s0, 0), pack_acc8(s0, 1), pack_acc8(s1, 0), pack_acc8(s1, 1)};
     static_for<4>([&](auto ks4c) {
       constexpr int ks4 = decltype(ks4c)::value;

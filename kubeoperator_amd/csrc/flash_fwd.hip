@@ -475,7 +475,7 @@ int flash_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o,
   const float sl2 = scale * 1.4426950408889634f;
   static const int variant = [] {
     const char* e = getenv("KOP_FWD_VARIANT");
-    return e ? atoi(e) : 9;
+    return e ? atoi(e) : 8;
   }();
   if (S % 256 == 0 && variant >= 8) {
     if (D == 128) {

@@ -476,6 +476,7 @@ def m_setup(ctx: ModuleContext, a: dict) -> dict:
         "ansible_devices": {k[7:]: {"size": _int(v)} for k, v in kv.items() if k.startswith("device_")},
     }
     ctx.facts_out.update(facts)
+    ctx.facts_out["ansible_facts"] = {k[len("ansible_"):]: v for k, v in facts.items()}
     return {"changed": False, "ansible_facts": facts, "failed": r.rc != 0 and not kv}
 
 

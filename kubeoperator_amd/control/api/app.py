@@ -1071,6 +1071,12 @@ def create_app() -> FastAPI:
             p = os.path.join(UI_DIR, "index.html")
         return FileResponse(p)
 
+    @app.get("/metrics")
+    def prometheus_metrics():
+        from ..runtime import metrics
+
+        return Response(metrics.exposition(), media_type="text/plain; version=0.0.4")
+
     @app.get("/healthz")
     def healthz():
         return {"ok": True, "time": time.time()}

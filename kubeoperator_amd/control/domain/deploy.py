@@ -18,10 +18,11 @@ idempotent), and ``timedelta`` is recorded in float seconds -- the cluster-creat
 from __future__ import annotations
 
 import logging
+import time
 
 from sqlalchemy import select
 
-from ..runtime import jobs
+from ..runtime import jobs, metrics
 from ..store import models as M
 from ..store.db import session_scope
 from . import clusters, context, plan
@@ -128,9 +129,17 @@ class _Exec:
         self.save()
 
     def update_step(self, name: str, status: str):
+        """Step status + timing: ``start`` / ``end`` epoch seconds and ``seconds`` (exported as metrics)."""
+        now = time.time()
         for i, st in enumerate(self.steps):
             if st["name"] == name:
                 st["status"] = status
+                if status == "running":
+                    st["start"] = now
+                elif status in ("success", "error") and "start" in st:
+                    st["end"] = now
+                    st["seconds"] = round(now - st["start"], 3)
+                    metrics.STEP_SECONDS.labels(self.operation, name, status).observe(st["seconds"])
                 self.save(current_step=i)
 
     def run_playbooks(self, ev: dict) -> dict:
@@ -189,6 +198,7 @@ def start(execution_id: str, logger=None) -> dict:
     ex.save(state="SUCCESS" if ok else "FAILURE", date_end=t1, timedelta=(t1 - t0).total_seconds(),
             result_summary=clusters._jsonable(result.get("summary", {})),
             result_raw=clusters._jsonable({k: v for k, v in (result.get("raw") or {}).items() if k != "ok"}))
+    metrics.EXECUTION_SECONDS.labels(op, "SUCCESS" if ok else "FAILURE").observe((t1 - t0).total_seconds())
     _notify(c, op, ok)
     return {"success": ok, "timedelta": (t1 - t0).total_seconds()}
 

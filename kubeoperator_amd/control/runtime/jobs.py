@@ -127,6 +127,9 @@ def run_job(job: M.Job) -> dict:
     lg.close()
     with session_scope() as s:
         s.execute(update(M.Job).where(M.Job.id == job.id).values(state=state, result=result, date_end=M.now()))
+    from . import metrics
+
+    metrics.JOBS_TOTAL.labels(job.name, state).inc()
     return {"state": state, "result": result}
 
 

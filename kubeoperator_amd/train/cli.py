@@ -30,6 +30,7 @@ def main(argv=None) -> int:
     ap.add_argument("--resume", action="store_true")
     ap.add_argument("--log-every", type=int, default=1)
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--gemm-tuning", default="use", choices=["off", "use", "tune"])
     a = ap.parse_args(argv)
 
     import torch
@@ -40,6 +41,9 @@ def main(argv=None) -> int:
     from .trainer import TrainConfig, Trainer, lr_at
 
     info = init_distributed(a.device)
+    from . import gemm_tuning
+
+    gemm_tuning.setup(a.gemm_tuning, rank=info.rank)
     tc = TrainConfig(model=a.model, micro_batch=a.mbs, seq_len=a.seq, grad_accum=a.accum, lr=a.lr,
                      warmup_steps=a.warmup, total_steps=a.steps, dp_mode=a.dp, bucket_mb=a.bucket_mb)
     tr = Trainer(tc, info)

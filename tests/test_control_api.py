@@ -176,3 +176,19 @@ def test_ui_served(control):
     c = TestClient(create_app())
     r = c.get("/ui/")
     assert r.status_code == 200 and "<html" in r.text.lower()
+
+
+def test_prometheus_metrics(client, control):
+    from kubeoperator_amd.control.domain import deploy
+    _register_hosts(client)
+    client.post("/api/v1/clusters/", json={"name": "mx", "template": "single-master",
+                                          "nodes": [{"name": "m1", "host": "m1", "roles": ["master"]},
+                                                    {"name": "w1", "host": "w1", "roles": ["worker"]}]})
+    e = deploy.create("mx", "install", run="inline")
+    assert e["state"] == "SUCCESS"
+    assert all("seconds" in s for s in e["steps"])
+    text = TestClient(create_app()).get("/metrics").text
+    assert 'kubeoperator_execution_seconds_count{operation="install",state="SUCCESS"}' in text
+    assert 'kubeoperator_step_seconds_count{operation="install",status="success",step="master"}' in text
+    assert 'kubeoperator_clusters{status="RUNNING"} 1.0' in text
+    assert 'kubeoperator_gpus{model="AMD Instinct MI355X"}' in text

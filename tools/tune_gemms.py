@@ -3,7 +3,7 @@ with a progress line per shape (a long silent tuning run looks hung to the job r
 
 1. one training step with TunableOp recording (not tuning) every GEMM it calls;
 2. each recorded GEMM is tuned on its own (max KOP_TUNE_MS ms / KOP_TUNE_ITERS iterations per solution);
-3. the winners are written to kubeoperator_amd/tuning/tunableop_results_gfx950.csv, which bench.py and the
+3. the winners are written (at exit) to kubeoperator_amd/tuning/tunableop_results_gfx950.csv, which bench.py and the
    trainer load read-only (``--gemm-tuning use``).
 
 Usage (one MI355X): python tools/tune_gemms.py [--model llama3_8b --seq 8192 --mbs 1]
@@ -71,8 +71,7 @@ def main():
         tun._process_single_offline_gemm(ln, dev)
         torch.cuda.synchronize()
         print(f"[{i + 1}/{len(lines)}] {time.time() - t0:6.1f}s {ln.strip()[:160]}", flush=True)
-        tun.write_file()
-    tun.write_file()
+    # TunableOp writes every tuned result to the results file when the process exits
     res = tun.get_results()
     print(f"wrote {len(res)} tuned results to {out}", flush=True)
     for r in res:

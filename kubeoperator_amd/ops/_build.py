@@ -111,10 +111,11 @@ def build_native(force: bool = False) -> list[str]:
 
     out = []
     py_inc = sysconfig.get_paths()["include"]
+    hdr = max((os.path.getmtime(h) for h in glob.glob(os.path.join(NATIVE_DIR, "*.h"))), default=0.0)
     for src in sorted(glob.glob(os.path.join(NATIVE_DIR, "*.cpp"))):
         so = os.path.splitext(src)[0] + ".so"
         out.append(so)
-        if not force and os.path.exists(so) and os.path.getmtime(so) >= os.path.getmtime(src):
+        if not force and os.path.exists(so) and os.path.getmtime(so) >= max(os.path.getmtime(src), hdr):
             continue
         tmp = so + ".tmp"
         _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-fvisibility=hidden",

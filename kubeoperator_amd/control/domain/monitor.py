@@ -230,10 +230,44 @@ def search_events(cluster_name: str, limit: int = 100, offset: int = 0, type_: s
 
 
 # ------------------------------------------------------------------------------------------- health
+GPU_TEMP_LIMIT_C = 105.0  # MI355X junction temperature above which the node is flagged
+
+
+def gpu_condition(node: dict, prom) -> dict:
+    """``AMDGPUHealthy`` node condition (new: the reference only counts GPUs). Unhealthy when the device
+    plugin advertises fewer ``amd.com/gpu`` than the node has, or the device-metrics exporter reports
+    uncorrectable ECC errors, an unhealthy device (``gpu_health`` 0) or a junction temperature over the limit."""
+    st = node.get("status", {})
+    cap = int(st.get("capacity", {}).get("amd.com/gpu", 0) or 0)
+    alloc = int(st.get("allocatable", {}).get("amd.com/gpu", 0) or 0)
+    problems = []
+    if cap and alloc < cap:
+        problems.append(f"{cap - alloc} of {cap} GPUs not allocatable")
+    if prom is not None and cap:
+        ip = next((a["address"] for a in st.get("addresses", []) if a.get("type") == "InternalIP"), "")
+        inst = f'instance=~"{ip}:.*"'
+        try:
+            ecc = prom.scalar(f"sum(gpu_ecc_uncorrect_total{{{inst}}})", 0.0)
+            unhealthy = prom.scalar(f"count(gpu_health{{{inst}}} == 0)", 0.0)
+            temp = prom.scalar(f"max(gpu_junction_temperature{{{inst}}})", 0.0)
+        except httpx.HTTPError:
+            ecc = unhealthy = temp = 0.0
+        if ecc > 0:
+            problems.append(f"{int(ecc)} uncorrectable ECC errors")
+        if unhealthy > 0:
+            problems.append(f"{int(unhealthy)} GPUs report unhealthy")
+        if temp > GPU_TEMP_LIMIT_C:
+            problems.append(f"junction temperature {temp:.0f} C > {GPU_TEMP_LIMIT_C:.0f} C")
+    return {"type": "AMDGPUHealthy", "status": "False" if problems else "True",
+            "message": "; ".join(problems) or f"{alloc} GPUs healthy", "reason": "GPUFault" if problems else "",
+            "lastTransitionTime": None}
+
+
 def node_health(cluster_name: str) -> list[dict]:
-    """Node conditions + nodeInfo from the k8s API into the node rows (reference node_health.py:10-56)."""
+    """Node conditions + nodeInfo from the k8s API into the node rows (reference node_health.py:10-56),
+    plus an ``AMDGPUHealthy`` condition on GPU nodes."""
     c = clusters.get_cluster(cluster_name)
-    k8s, _, _ = _clients(c)
+    k8s, prom, _ = _clients(c)
     out = []
     nodes = {n["metadata"]["name"]: n for n in k8s.get("/api/v1/nodes").get("items", [])}
     with session_scope() as s:
@@ -244,6 +278,8 @@ def node_health(cluster_name: str) -> list[dict]:
             else:
                 row.conditions = [{k: cd.get(k) for k in ("type", "status", "message", "reason", "lastTransitionTime")}
                                   for cd in n["status"].get("conditions", [])]
+                if n["status"].get("capacity", {}).get("amd.com/gpu"):
+                    row.conditions = row.conditions + [gpu_condition(n, prom)]
                 row.info = n["status"].get("nodeInfo", {}) | {"allocatable": n["status"].get("allocatable", {})}
             out.append({"name": row.name, "conditions": row.conditions})
     return out

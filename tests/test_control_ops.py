@@ -251,6 +251,10 @@ class _K8s:
 
 class _Prom:
     def scalar(self, q, default=0.0):
+        if "gpu_ecc_uncorrect_total" in q:
+            return 2.0
+        if "gpu_health" in q or "gpu_junction_temperature" in q:
+            return 0.0
         if "gpu_gfx_activity" in q and q.startswith("avg"):
             return 87.0
         if "count(gpu_gfx_activity" in q:
@@ -279,5 +283,9 @@ def test_monitor_with_stub_clients(control):
     g = monitor.grade("mon")
     ids = {r["id"] for r in g["results"][0]["results"] if not r["success"]}
     assert {"tagNotSpecified", "gpuLimitMissing", "livenessProbeMissing"} <= ids
+    cond = monitor.gpu_condition(_K8s().get("/api/v1/nodes")["items"][0], _Prom())
+    assert cond["type"] == "AMDGPUHealthy" and cond["status"] == "False" and "ECC" in cond["message"]
+    ok = monitor.gpu_condition(_K8s().get("/api/v1/nodes")["items"][0], None)
+    assert ok["status"] == "True"
     monitor.record_availability("mon", 99.0)
     assert monitor.availability_history(clusters.get_cluster("mon").id)[0]["available_rate"] == 99.0

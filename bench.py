@@ -36,6 +36,8 @@ def main() -> int:
     ap.add_argument("--device", default="auto")
     ap.add_argument("--gemm-tuning", default="use", choices=["off", "use", "tune"],
                     help="hipBLASLt solution selection: committed TunableOp winners (use), heuristic (off), re-tune")
+    ap.add_argument("--overlap-opt", type=int, default=1, choices=[0, 1],
+                    help="run AdamW on its own stream, gated per bucket into the next forward (1) or serially (0)")
     args = ap.parse_args()
 
     import torch
@@ -52,7 +54,8 @@ def main() -> int:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the real world size",
               file=sys.stderr)
     tc = TrainConfig(model=args.model, micro_batch=args.mbs, seq_len=args.seq, grad_accum=args.accum,
-                     dp_mode=args.dp, bucket_mb=args.bucket_mb, warmup_steps=10, total_steps=1000)
+                     dp_mode=args.dp, bucket_mb=args.bucket_mb, warmup_steps=10, total_steps=1000,
+                     overlap_optimizer=bool(args.overlap_opt))
     trainer = Trainer(tc, info)
     data = SyntheticTokens(trainer.cfg.vocab_size, args.mbs, args.seq, info.device, seed=tc.seed, rank=info.rank)
     cuda = info.device.type == "cuda"
@@ -108,6 +111,7 @@ def main() -> int:
                 "seq_len": args.seq,
                 "parallelism": f"dp{world}" + ("-zero1" if args.dp == "zero1" and world > 1 else ""),
                 "optimizer": "fused AdamW (fp32 master/moments), grad clip 1.0",
+                "optimizer_overlap": bool(args.overlap_opt),
             },
             "tflops_per_gpu": round(flops_tok * value / world / 1e12, 1),
             "last_loss": round(last_loss, 4),

@@ -163,6 +163,17 @@ std::vector<Tensor> cross_entropy_fwd_(const Tensor& logits, const Tensor& targe
   return {loss, lse, scale};
 }
 
+// ------------------------------------------------------------------ transpose
+void transpose_(const Tensor& in, const Tensor& out) {
+  check_bf16(in, "in");
+  check_bf16(out, "out");
+  check_rows(in, "in");
+  check_rows(out, "out");
+  TORCH_CHECK(out.size(0) == in.size(1) && out.size(1) == in.size(0), "out must be [in.cols, in.rows]");
+  rc(kop::transpose2d(bp(in), bp(out), in.size(0), in.size(1), in.stride(0), out.stride(0), cur_stream()),
+     "transpose (rows and columns must be multiples of 8)");
+}
+
 // ------------------------------------------------------------------ optimizer
 void adamw_(const Tensor& p, const Tensor& g, const Tensor& master, const Tensor& m, const Tensor& v, double lr,
             double b1, double b2, double eps, double wd, int64_t step, double gscale,
@@ -253,6 +264,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("cross_entropy_fwd_", &cross_entropy_fwd_);
+  m.def("transpose_", &transpose_);
   m.def("adamw_", &adamw_);
   m.def("grad_sumsq_", &grad_sumsq_);
   m.def("clip_coef_", &clip_coef_);

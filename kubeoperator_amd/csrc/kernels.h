@@ -36,6 +36,9 @@ int adamw_step(bf16_t* p, const bf16_t* g, float* master, float* m, float* v, in
 int grad_sumsq(const bf16_t* g, int64_t n, float* out, hipStream_t stream);
 int clip_coef(const float* sumsq, float max_norm, float* coef, float* norm_out, hipStream_t stream);
 
+// transpose.hip
+int transpose2d(const bf16_t* in, bf16_t* out, int64_t R, int64_t C, int64_t ldi, int64_t ldo, hipStream_t stream);
+
 // flash_attn.hip
 int flash_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int S, int Hq,
                    int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, float scale, bool causal,

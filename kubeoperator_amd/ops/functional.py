@@ -12,6 +12,7 @@ launch the bucket's collective immediately -- no AccumulateGrad pass, no extra c
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -42,11 +43,47 @@ def _sink(w: torch.Tensor, produce):
     return None
 
 
+def _gate(*ws):
+    """Order the compute stream after the optimizer stream's update of these weights (parallel.flat gates)."""
+    for w in ws:
+        h = getattr(w, "_kop_hooks", None)
+        if h is not None:
+            h.store.await_param(w)
+
+
 def _mm_into(a, b, out, accumulate):
     if accumulate:
         out.addmm_(a, b)
     else:
         torch.mm(a, b, out=out)
+
+
+# weight gradients dW = dY^T X through the forward ("TN") GEMM layout: hipBLASLt runs the strided "NT"
+# form at ~1.15 PF/s and the K-contiguous form at ~1.55 PF/s on MI355X; two HIP transposes at HBM speed
+# cost far less than the difference (tools/bench_gemm_layouts.py, csrc/transpose.hip).
+_DW_LAYOUT = os.environ.get("KOP_DW_LAYOUT", "tn")
+_DW_TN_MIN_ROWS = 1024
+
+
+def _rows_ok(t: torch.Tensor) -> bool:
+    return (t.dtype == torch.bfloat16 and t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 8 == 0
+            and t.shape[1] % 8 == 0 and t.data_ptr() % 16 == 0)
+
+
+def transpose(x: torch.Tensor) -> torch.Tensor:
+    """Contiguous [C, R] copy of a bf16 [R, C] row view (HIP kernel)."""
+    out = torch.empty(x.shape[1], x.shape[0], dtype=x.dtype, device=x.device)
+    _lib().transpose_(x, out)
+    return out
+
+
+def _dw_into(dy2, x2, out, accumulate):
+    """out (+)= dy2^T @ x2, the reduction running over the token rows."""
+    if (_DW_LAYOUT == "tn" and dy2.shape[0] >= _DW_TN_MIN_ROWS and dy2.shape[0] % 8 == 0 and _rows_ok(dy2)
+            and _rows_ok(x2)):
+        _mm_into(transpose(dy2), transpose(x2).t(), out, accumulate)
+    else:
+        _mm_into(dy2.t(), x2, out, accumulate)
 
 
 # ---------------------------------------------------------------------------------------------------
@@ -69,7 +106,7 @@ class _Linear(Function):
         x2, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, w.shape[0])
         dx = torch.mm(dy2, w).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
-        dw = _sink(w, lambda out, acc: _mm_into(dy2.t(), x2, out, acc)) if ctx.needs_input_grad[1] else None
+        dw = _sink(w, lambda out, acc: _dw_into(dy2, x2, out, acc)) if ctx.needs_input_grad[1] else None
         db = None
         if ctx.has_b and ctx.needs_input_grad[2]:
             def prod(out, acc):
@@ -85,6 +122,7 @@ class _Linear(Function):
 def linear(x, w, b=None):
     if not x.is_cuda:
         return F.linear(x, w, b)
+    _gate(w, b)
     return _Linear.apply(x, w, b)
 
 
@@ -149,6 +187,7 @@ def rms_norm(x, w, eps=1e-5, residual=None):
     if not x.is_cuda:
         y, s = ref.rms_norm_ref(x, w, eps, residual)
         return (y, s) if residual is not None else y
+    _gate(w)
     return _Norm.apply(x, residual, w, None, eps, False)
 
 
@@ -156,6 +195,7 @@ def layer_norm(x, w, b, eps=1e-5, residual=None):
     if not x.is_cuda:
         y, s = ref.layer_norm_ref(x, w, b, eps, residual)
         return (y, s) if residual is not None else y
+    _gate(w, b)
     return _Norm.apply(x, residual, w, b, eps, True)
 
 
@@ -305,6 +345,7 @@ class _Embedding(Function):
 def embedding(ids, w):
     if not w.is_cuda:
         return F.embedding(ids, w)
+    _gate(w)
     return _Embedding.apply(ids, w)
 
 
@@ -333,7 +374,7 @@ class _LMHeadCE(Function):
         dw = None
         if ctx.needs_input_grad[1]:
             xg = x2 * g
-            dw = _sink(w, lambda out, acc: _mm_into(dlogits.t(), xg, out, acc))
+            dw = _sink(w, lambda out, acc: _dw_into(dlogits, xg, out, acc))
         return dx, dw, None, None
 
 
@@ -342,4 +383,5 @@ def cross_entropy_lmhead(x, w, targets, ignore_index=-100):
     if not x.is_cuda:
         logits = F.linear(x.reshape(-1, x.shape[-1]), w)
         return F.cross_entropy(logits.float(), targets.reshape(-1), ignore_index=ignore_index)
+    _gate(w)
     return _LMHeadCE.apply(x, w, targets, ignore_index)

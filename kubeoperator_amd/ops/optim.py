@@ -6,6 +6,12 @@ and keeps fp32 master weights, exp_avg and exp_avg_sq for all segments in three 
 One ``adamw_`` kernel launch per segment (a handful per step: one per weight-decay region, or one per
 ZeRO-1 bucket shard). Gradient clipping is computed on device (sum of squares -> clip coefficient) and fed
 to the kernel as a device scalar, so a step never synchronises with the host.
+
+Overlap (``store`` given, GPU): the update runs on the optimizer's own HIP stream, one launch per bucket
+in the order the next forward pass reads the buckets (``FlatParamStore.use_order``), and each launch
+publishes a gate for its bucket (an event, or what ``on_segment`` returns -- the ZeRO-1 all-gather work).
+The forward kernels wait only for the gate of the bucket they read, so the HBM-bound AdamW (~28 B/param)
+runs underneath the next step's compute-bound forward instead of in its own serial phase.
 """
 from __future__ import annotations
 
@@ -20,12 +26,13 @@ class Segment:
     param: torch.Tensor  # bf16 view (flat)
     grad: torch.Tensor   # bf16 view (flat), same numel
     weight_decay: float
+    bucket: int = -1     # flat-store bucket this segment belongs to (for overlap gates)
 
 
 class FusedAdamW:
     def __init__(self, segments: list[Segment], lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
                  weight_decay: float = 0.1, max_grad_norm: float = 1.0, grad_scale: float = 1.0,
-                 norm_allreduce=None):
+                 norm_allreduce=None, store=None, on_segment=None):
         # a segment's weight_decay of None means "the optimizer's default"
         for sg in segments:
             if sg.weight_decay is None:
@@ -54,6 +61,10 @@ class FusedAdamW:
         self._sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
         self._coef = torch.ones(1, dtype=torch.float32, device=dev)
         self.last_grad_norm = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.store = store
+        self.on_segment = on_segment  # callable(Segment) -> gate or None, runs on the optimizer stream
+        self.overlap = store is not None and dev.type == "cuda" and all(sg.bucket >= 0 for sg in segments)
+        self._stream = torch.cuda.Stream(device=dev) if self.overlap else None
 
     # -------------------------------------------------------------------------------------------
     def state_bytes(self) -> int:
@@ -91,20 +102,41 @@ class FusedAdamW:
             self.last_grad_norm.copy_(nrm)
             self._coef.copy_(torch.clamp(self.max_grad_norm / (nrm + 1e-6), max=1.0))
 
+    def _launch_order(self) -> list[int]:
+        pos = {b: i for i, b in enumerate(self.store.use_order)}
+        return sorted(range(len(self.segments)), key=lambda k: (pos.get(self.segments[k].bucket, 1 << 30), k))
+
     def step(self, lr: float | None = None):
         lr = self.lr if lr is None else lr
         self.step_count += 1
+        if self.store is not None:
+            self.store.await_all()
         self.clip()
         if self._native():
             from . import load
 
             lib = load()
-            for s, (a, b) in zip(self.segments, self._views):
-                if b == a:
-                    continue
-                lib.adamw_(s.param.reshape(-1), s.grad.reshape(-1), self.master[a:b], self.exp_avg[a:b],
-                           self.exp_avg_sq[a:b], lr, self.b1, self.b2, self.eps, s.weight_decay, self.step_count,
-                           self.grad_scale, self._coef)
+
+            def launch(k):
+                s, (a, b) = self.segments[k], self._views[k]
+                if b > a:
+                    lib.adamw_(s.param.reshape(-1), s.grad.reshape(-1), self.master[a:b], self.exp_avg[a:b],
+                               self.exp_avg_sq[a:b], lr, self.b1, self.b2, self.eps, s.weight_decay,
+                               self.step_count, self.grad_scale, self._coef)
+
+            if not self.overlap:
+                for k in range(len(self.segments)):
+                    launch(k)
+                return
+            self._stream.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self._stream):
+                for k in self._launch_order():
+                    launch(k)
+                    gate = self.on_segment(self.segments[k]) if self.on_segment is not None else None
+                    if gate is None:
+                        gate = torch.cuda.Event()
+                        gate.record(self._stream)
+                    self.store.set_gate(self.segments[k].bucket, gate)
         else:
             t = self.step_count
             bc1 = 1 - self.b1 ** t
@@ -120,10 +152,14 @@ class FusedAdamW:
 
     # checkpointing -------------------------------------------------------------------------------
     def state_dict(self):
+        if self.store is not None:
+            self.store.await_all()
         return {"step": self.step_count, "master": self.master, "exp_avg": self.exp_avg,
                 "exp_avg_sq": self.exp_avg_sq, "lr": self.lr}
 
     def load_state_dict(self, sd):
+        if self.store is not None:
+            self.store.await_all()
         self.step_count = int(sd["step"])
         self.master.copy_(sd["master"])
         self.exp_avg.copy_(sd["exp_avg"])

@@ -45,6 +45,7 @@ class DataParallel:
         self.comm_bytes = 0
         store.on_ready = self._on_ready
         self._nccl = info.backend == "nccl"
+        self.overlapped = False  # set once the optimizer publishes ZeRO-1 gathers itself
 
     # -------------------------------------------------------------------------------------------
     def broadcast_params(self) -> None:
@@ -76,14 +77,33 @@ class DataParallel:
         st = self.store
         wd_of = {True: None, False: 0.0}
         segs = []
-        if self.mode == "allreduce" or self.world == 1:
-            for a, e, decay in st.regions():
-                segs.append(Segment(st.params[a:e], st.grads[a:e], wd_of[decay]))
-        else:
-            for b in st.buckets:
-                a, e = b.piece(self.rank, self.world)
-                segs.append(Segment(st.params[a:e], st.grads[a:e], wd_of[b.decay]))
+        for b in st.buckets:
+            a, e = (b.start, b.end) if self.mode == "allreduce" or self.world == 1 else b.piece(self.rank, self.world)
+            segs.append(Segment(st.params[a:e], st.grads[a:e], wd_of[b.decay], b.index))
         return segs
+
+    def publish_segment(self, seg: Segment):
+        """Optimizer-overlap hook, called on the optimizer stream right after a bucket's AdamW launch.
+        ZeRO-1: start the bucket's in-place all-gather there and hand its work back as the bucket's gate."""
+        if self.mode != "zero1" or self.world == 1:
+            return None
+        self.overlapped = True
+        b = self.store.buckets[seg.bucket]
+        a, e = b.piece(self.rank, self.world)
+        return self._gather(b, a, e, async_op=True)
+
+    def _gather(self, b: Bucket, a: int, e: int, async_op: bool):
+        st = self.store
+        full = st.params[b.start:b.end]
+        if self._nccl:
+            return dist.all_gather_into_tensor(full, st.params[a:e], async_op=async_op)
+        n = e - a
+        outs = [full[i * n:(i + 1) * n] for i in range(self.world)]
+        tmp = [torch.empty_like(o) for o in outs]
+        dist.all_gather(tmp, st.params[a:e].clone())
+        for o, t in zip(outs, tmp):
+            o.copy_(t)
+        return None
 
     def norm_allreduce(self):
         if self.mode == "zero1" and self.world > 1:
@@ -92,21 +112,14 @@ class DataParallel:
 
     def after_step(self) -> None:
         """ZeRO-1: all-gather the updated bf16 parameter pieces back into every rank's flat buffer."""
-        if self.mode != "zero1" or self.world == 1:
+        if self.mode != "zero1" or self.world == 1 or self.overlapped:
             return
         st = self.store
         for b in st.buckets:
             a, e = b.piece(self.rank, self.world)
-            full = st.params[b.start:b.end]
-            if self._nccl:
-                self._gather_works.append(dist.all_gather_into_tensor(full, st.params[a:e], async_op=True))
-            else:
-                n = (e - a)
-                outs = [full[i * n:(i + 1) * n] for i in range(self.world)]
-                tmp = [torch.empty_like(o) for o in outs]
-                dist.all_gather(tmp, st.params[a:e].clone())
-                for o, t in zip(outs, tmp):
-                    o.copy_(t)
+            w = self._gather(b, a, e, async_op=self._nccl)
+            if w is not None:
+                self._gather_works.append(w)
         self.wait_params()
 
     def wait_params(self) -> None:

@@ -17,6 +17,12 @@ decided once, MI355X-first:
 
 Readiness is counted per parameter *use* (tied embeddings are used twice): when all uses of all
 parameters of a bucket have written their gradient, the bucket's ``on_ready`` callback fires.
+
+Forward gates (optimizer overlap): the fused AdamW may run on its own HIP stream, bucket by bucket in the
+order the forward pass first touches them, and publish a *gate* per bucket (an event, or the RCCL
+all-gather work under ZeRO-1). The kernels' Python wrappers call ``await_param`` on every weight they read,
+which makes the compute stream wait for that bucket's gate only -- so the memory-bound optimizer of step k
+streams underneath the compute-bound forward GEMMs of step k+1 instead of running alone.
 """
 from __future__ import annotations
 
@@ -59,6 +65,13 @@ class Bucket:
     def piece(self, rank: int, world: int) -> tuple[int, int]:
         n = self.numel // world
         return self.start + rank * n, self.start + (rank + 1) * n
+
+
+def _resolve(gate) -> None:
+    if isinstance(gate, torch.cuda.Event):
+        torch.cuda.current_stream().wait_event(gate)
+    else:  # torch.distributed work: wait() orders the current stream after the collective
+        gate.wait()
 
 
 class GradHooks:
@@ -133,6 +146,9 @@ class FlatParamStore:
         self._bucket_of: dict[int, Bucket] = {}
         self._param_by_name: dict[str, nn.Parameter] = {}
         self.on_ready = None  # callable(Bucket)
+        self.gates: dict[int, object] = {}  # bucket index -> torch.cuda.Event | collective work
+        self.use_order: list[int] = []  # bucket indices in the order the forward pass first reads them
+        self._used: set[int] = set()
         name_to_bucket = {nm: b for b in self.buckets for nm in b.names}
         for s in specs:
             n = s.param.numel()
@@ -205,6 +221,27 @@ class FlatParamStore:
         b.pending -= 1
         if b.pending == 0 and self.on_ready is not None:
             self.on_ready(b)
+
+    # forward gates ------------------------------------------------------------------------------
+    def await_param(self, p) -> None:
+        """Called before a kernel reads parameter ``p``: wait (on the current stream) for its bucket's gate."""
+        b = self._bucket_of.get(id(p))
+        if b is None:
+            return
+        if b.index not in self._used:
+            self._used.add(b.index)
+            self.use_order.append(b.index)
+        g = self.gates.pop(b.index, None)
+        if g is not None:
+            _resolve(g)
+
+    def set_gate(self, index: int, gate) -> None:
+        self.gates[index] = gate
+
+    def await_all(self) -> None:
+        """Resolve every outstanding gate (before checkpointing, evaluation, or the next optimizer step)."""
+        for i in list(self.gates):
+            _resolve(self.gates.pop(i))
 
     def zero_grads(self) -> None:
         self.grads.zero_()

@@ -31,6 +31,7 @@ def main(argv=None) -> int:
     ap.add_argument("--log-every", type=int, default=1)
     ap.add_argument("--device", default="auto")
     ap.add_argument("--gemm-tuning", default="use", choices=["off", "use", "tune"])
+    ap.add_argument("--overlap-opt", type=int, default=1, choices=[0, 1])
     a = ap.parse_args(argv)
 
     import torch
@@ -45,7 +46,7 @@ def main(argv=None) -> int:
 
     gemm_tuning.setup(a.gemm_tuning, rank=info.rank)
     tc = TrainConfig(model=a.model, micro_batch=a.mbs, seq_len=a.seq, grad_accum=a.accum, lr=a.lr,
-                     warmup_steps=a.warmup, total_steps=a.steps, dp_mode=a.dp, bucket_mb=a.bucket_mb)
+                     warmup_steps=a.warmup, total_steps=a.steps, dp_mode=a.dp, bucket_mb=a.bucket_mb, overlap_optimizer=bool(a.overlap_opt))
     tr = Trainer(tc, info)
     if a.resume and a.ckpt_dir:
         s = checkpoint.load(tr, a.ckpt_dir, info)

@@ -35,6 +35,7 @@ class TrainConfig:
     grad_clip: float = 1.0
     dp_mode: str = "allreduce"  # allreduce | zero1
     bucket_mb: int = 512
+    overlap_optimizer: bool = True  # AdamW on its own stream, gated per bucket into the next forward
     seed: int = 1234
     model_overrides: dict = field(default_factory=dict)
 
@@ -67,7 +68,9 @@ class Trainer:
         self.dp.broadcast_params()
         self.opt = FusedAdamW(self.dp.optimizer_segments(), lr=tc.lr, betas=tc.betas, eps=tc.eps,
                               weight_decay=tc.weight_decay, max_grad_norm=tc.grad_clip,
-                              grad_scale=self.dp.grad_scale / tc.grad_accum, norm_allreduce=self.dp.norm_allreduce())
+                              grad_scale=self.dp.grad_scale / tc.grad_accum, norm_allreduce=self.dp.norm_allreduce(),
+                              store=self.store if tc.overlap_optimizer else None,
+                              on_segment=self.dp.publish_segment)
         self.step = 0
         self.setup_seconds = time.time() - t0
 
@@ -94,6 +97,7 @@ class Trainer:
 
     # checkpoint -----------------------------------------------------------------------------------
     def state_dict(self):
+        self.store.await_all()
         return {"step": self.step, "train_config": self.tc.to_dict(), "model_config": self.cfg.to_dict(),
                 "params": self.store.params, "optimizer": self.opt.state_dict(), "world": self.info.world,
                 "rank": self.info.rank, "dp_mode": self.tc.dp_mode}
@@ -101,6 +105,7 @@ class Trainer:
     def load_state_dict(self, sd):
         if sd["world"] != self.info.world and self.tc.dp_mode == "zero1":
             raise ValueError("ZeRO-1 checkpoints are sharded per rank: resume with the same world size")
+        self.store.await_all()
         self.store.params.copy_(sd["params"])
         self.opt.load_state_dict(sd["optimizer"])
         self.step = int(sd["step"])

@@ -258,3 +258,28 @@ def test_rope_attention_end_to_end_grad():
     (oc * do.cpu().float()).sum().backward()
     assert rel_err(o.cpu(), oc) < 2e-2
     assert rel_err(qkv.grad.cpu(), qc.grad) < 3e-2
+
+
+@pytest.mark.parametrize("R,C", [(64, 64), (8192, 6144), (104, 200), (8, 4104)])
+def test_transpose_exact(R, C):
+    from kubeoperator_amd.ops.functional import transpose
+
+    x = torch.randn(R, C + 16, device=DEV).to(torch.bfloat16)[:, 8:C + 8]  # strided, 16-B aligned rows
+    y = transpose(x)
+    assert y.shape == (C, R) and y.is_contiguous()
+    assert torch.equal(y, x.t())
+
+
+def test_weight_grad_tn_layout_matches_nt():
+    import kubeoperator_amd.ops.functional as kf
+
+    torch.manual_seed(11)
+    T, N, K = 2048, 768, 512
+    x = torch.randn(T, K, device=DEV).to(torch.bfloat16)
+    dy = torch.randn(T, N, device=DEV).to(torch.bfloat16)
+    out = torch.empty(N, K, device=DEV, dtype=torch.bfloat16)
+    kf._dw_into(dy, x, out, False)
+    ref = dy.float().t() @ x.float()
+    assert rel_err(out, ref) < 1e-2
+    kf._dw_into(dy, x, out, True)
+    assert rel_err(out, 2 * ref) < 1e-2

@@ -271,4 +271,5 @@ PYBIND11_MODULE(_C, m) {
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd_workspace", &flash_attn_bwd_workspace);
   m.def("flash_attn_bwd", &flash_attn_bwd);
+  m.def("flash_attn_set_dq_variant", [](int64_t v) { return (int64_t)kop::flash_attn_set_dq_variant((int)v); });
 }

@@ -22,6 +22,12 @@
 //       is directly the B operand of dQ^T += K^T.dS^T (K^T by transposed reads of the K tile).
 //       dQ is written once, in bf16, straight into the strided dQKV gradient.
 //   fa_bwd_finalize_kernel : dK, dV = bf16(sum over the GQA group of the per-q-head partials).
+//
+// Default since the dS variant (KOP_DQ_VARIANT 10): the dK/dV kernel also stores its bf16 dS tiles
+// ([B, Hq, S, S], ~1 TB/s of extra writes it hides under its MFMA work) and fa_bwd_dq_ds_kernel computes
+// dQ = scale * dS.K from them -- one MFMA product plus an HBM stream instead of three products; at
+// Llama-3-8B shape the backward drops from 3.31 to 2.89 ms (profiles/r1_attn_dq10_bench.log). The
+// buffer is capped at 16 GiB; longer sequences fall back to the recompute kernels.
 #include "attn_common.h"
 #include "kernels.h"
 
@@ -59,12 +65,18 @@ __global__ void __launch_bounds__(256) fa_bwd_delta_kernel(const bf16_t* __restr
 // =============================================================================================
 // dK / dV
 // =============================================================================================
-template <int D, int NW>
+// slot of key (k & 15) inside its 16-key group in the dS buffer: keys {0-3, 8-11, 4-7, 12-15} so lane half hh
+// of the dQ kernel reads the 8 keys {4hh..4hh+3, 8+4hh..8+4hh+3} of its MFMA B fragment as one 16-B chunk
+__device__ __forceinline__ int ds_slot(int key) {
+  return (key & ~15) | (key & 3) | ((key & 4) << 1) | ((key & 8) >> 1);
+}
+
+template <int D, int NW, bool WDS = false>
 __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
-    float* __restrict__ dk_part, float* __restrict__ dv_part, int B, int S, int Hq, int Hkv, int64_t qs, int64_t ks,
-    int64_t vs, int64_t dos, float scale, int causal) {
+    float* __restrict__ dk_part, float* __restrict__ dv_part, bf16_t* __restrict__ ds, int B, int S, int Hq,
+    int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t dos, float scale, int causal) {
   // LDS: the workgroup's K block (BN rows, read as the S = Q.K^T B operand) + a 2-deep ring of 32-query
   // stages {Q, dO, lse/delta}; 66 KiB at D = 128 so two workgroups share a CU (V^T stays in VGPRs).
   constexpr int BN = 32 * NW, BQ = 32, ROWB = D * 2;
@@ -223,6 +235,15 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
           dkacc[dt] = mfma32(cat44(t[4 * s + 2], t[4 * s + 3]), sb[s], dkacc[dt]);
         }
       });
+      if constexpr (WDS) {
+        // unscaled bf16 dS -> ds[b, hq, q, slot(key)]: per store the 32 keys of a row half-wave are 64
+        // contiguous bytes (the same rounding dK uses below)
+        // wave-uniform row pointer (SGPRs) + one 32-bit lane offset: no per-store 64-bit address VGPRs
+        const int loff = 4 * hh * S + ds_slot(key);
+        short* const dsw = reinterpret_cast<short*>(ds) + ((int64_t)(b * Hq + hq) * S + qs0) * S;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) dsw[(int64_t)((j & 3) + 8 * (j >> 2)) * S + loff] = sb[j >> 3][j & 7];
+      }
     }
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_barrier();  // stage is refilled by the next iteration's DMA
@@ -579,6 +600,113 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq8_kernel(
   }
 }
 
+// dQ from the materialised dS (KOP_DQ_VARIANT 10): dQ = scale * dS . K with dS written by the dK/dV kernel,
+// so neither S nor dP is recomputed (the recompute dQ kernels above redo 2 of their 3 MFMA products).
+// One workgroup = 8 waves = 256 queries of one (b, q-head), 64-key tiles: the K tile (read transposed, as
+// the forward reads V) and the [256 x 64] dS tile both arrive by LDS-DMA into a 3-slot ring; per 16-key
+// group a lane's B fragment dS^T is one ds_read_b128 of its row (keys are stored in MFMA order, ds_slot),
+// and dQ^T += K^T . dS^T accumulates in DT independent chains. The dS stream (half of B*Hq*S*S bf16 under
+// a causal mask) makes this kernel HBM-bound, ~3x cheaper than recomputing.
+template <int D>
+__global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __restrict__ ds, const bf16_t* __restrict__ k,
+                                                              bf16_t* __restrict__ dq, int B, int S, int Hq, int Hkv,
+                                                              int64_t ks, int64_t dqs, float scale, int causal) {
+  constexpr int NW = 8, BM = 256, BN = 64, ROWB = D * 2, NSLOT = 3;
+  constexpr int KT = BN * ROWB, DST = BM * BN * 2, SLOT = KT + DST;
+  constexpr int PPW = (KT / 1024) / NW + (DST / 1024) / NW;  // DMA pieces per wave per tile
+  static_assert((KT / 1024) % NW == 0 && (DST / 1024) % NW == 0, "tiles must split evenly over the waves");
+  constexpr int DT = D / 32, NR = 2 * DT;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hh = lane >> 5;
+  const int tq = (lane & 15) >> 2, tp = lane & 3, tg1 = (lane >> 4) & 1;
+  const int nqb = S / BM;
+  const int nwork = B * Hq * nqb;
+  const int work = xcd_remap(blockIdx.x, nwork);
+  const int qb = causal ? (nqb - 1 - work / (B * Hq)) : work / (B * Hq);
+  const int rest = work % (B * Hq);
+  const int b = rest / Hq, hq = rest % Hq;
+  const int kvh = hq / (Hq / Hkv);
+  const int q0 = qb * BM, q0w = q0 + wid * 32;
+  const int ntiles = causal ? (q0 + BM) / BN : S / BN;
+  const bf16_t* kbase = k + (int64_t)(b * S) * ks + kvh * D;
+  const bf16_t* dsbase = ds + ((int64_t)(b * Hq + hq) * S + q0) * S;
+  auto issue = [&](int t) {
+    char* sl = smem + (t % NSLOT) * SLOT;
+    dma_tile_a<ROWB, NW, BN>(sl, kbase + (int64_t)(t * BN) * ks, ks, wid, lane);
+    dma_tile_a<BN * 2, NW, BM>(sl + KT, dsbase + t * BN, S, wid, lane);
+  };
+  issue(0);
+  if (ntiles > 1) issue(1);
+
+  constexpr int RB = ROWB * 8;
+  // K^T transposed reads (as the forward's V^T): rows R0 + 4hh + tq (+8) at column block dt
+  const int kb_lane0 = 64 * (4 * hh + tq) + 16 * ((2 * tg1 + (tp >> 1)) ^ hh) + 8 * (tp & 1);
+  const int kb_lane1 = 64 * (4 * hh + tq) + 16 * ((2 * tg1 + (tp >> 1)) ^ (2 + hh)) + 8 * (tp & 1);
+  // dS row reads of row 32*wid + r at chunk 2*ks4 + hh in the sub-tiled [256][128 B] image
+  const int ds_lane0 = 4096 * wid + 1024 * (r >> 3) + 64 * (r & 7) + 16 * (hh ^ ((r >> 2) & 3));
+  const int ds_lane1 = 4096 * wid + 1024 * (r >> 3) + 64 * (r & 7) + 16 * ((2 + hh) ^ ((r >> 2) & 3));
+  f32x16 acc[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) acc[i] = f32x16{0};
+  const int qi = q0w + r;
+
+  for (int it = 0; it < ntiles; ++it) {
+    if (it + 1 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (it + 2 < ntiles) issue(it + 2);
+    const int kv0 = it * BN;
+    if (!causal || kv0 <= q0w + 31) {
+      const char* sl = smem + (it % NSLOT) * SLOT;
+      const uint32_t kb0 = lds_addr(sl) + kb_lane0, kb1 = lds_addr(sl) + kb_lane1;
+      const uint32_t db0 = lds_addr(sl + KT) + ds_lane0, db1 = lds_addr(sl + KT) + ds_lane1;
+      bf16x8 f[4];
+      static_for<4>([&](auto ks4c) {
+        constexpr int ks4 = decltype(ks4c)::value;
+        f[ks4] = lds_read8_off<512 * (ks4 >> 1)>((ks4 & 1) ? db1 : db0);
+      });
+      const bool diag = causal && kv0 + BN - 1 > q0w;
+      static_for<4>([&](auto ks4c) {
+        constexpr int ks4 = decltype(ks4c)::value;
+        constexpr int R0 = 16 * ks4;
+        bf16x4 t[NR];
+        static_for<DT>([&](auto dtc) {
+          constexpr int dt = decltype(dtc)::value;
+          t[2 * dt] = lds_tr_read_off<RB * (R0 >> 3) + 512 * dt>(((R0 >> 3) & 1) ? kb1 : kb0);
+          t[2 * dt + 1] = lds_tr_read_off<RB * ((R0 + 8) >> 3) + 512 * dt>((((R0 + 8) >> 3) & 1) ? kb1 : kb0);
+        });
+        wait_tr<NR, 0>(t);
+        bf16x8 fb = f[ks4];
+        if (diag) {  // keys past the query: zero (the dK/dV kernel never wrote fully masked 32x32 blocks)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const int key = kv0 + R0 + 4 * hh + (e & 3) + 8 * (e >> 2);
+            if (key > qi) fb[e] = 0;
+          }
+        }
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) acc[dt] = mfma32(cat44(t[2 * dt], t[2 * dt + 1]), fb, acc[dt]);
+      });
+    }
+    asm volatile("" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  bf16_t* dp = dq + (int64_t)(b * S + qi) * dqs + hq * D;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      u32x2 w;
+      w[0] = pack2(acc[dt][4 * g4] * scale, acc[dt][4 * g4 + 1] * scale);
+      w[1] = pack2(acc[dt][4 * g4 + 2] * scale, acc[dt][4 * g4 + 3] * scale);
+      *reinterpret_cast<u32x2*>(dp + dt * 32 + 8 * g4 + 4 * hh) = w;
+    }
+  }
+}
+
 // dk/dv = bf16(sum over the GQA group of the per-q-head partials)
 template <int D>
 __global__ void __launch_bounds__(256) fa_bwd_finalize_kernel(const float* __restrict__ dk_part,
@@ -613,9 +741,28 @@ __global__ void __launch_bounds__(256) fa_bwd_finalize_kernel(const float* __res
 // ---------------------------------------------------------------------------------------------
 constexpr int kBwdWaves = 4;
 
+static int g_dq_variant = -1;  // -1: read KOP_DQ_VARIANT on first use
+static int dq_variant() {
+  if (g_dq_variant < 0) {
+    const char* e = getenv("KOP_DQ_VARIANT");
+    g_dq_variant = e ? atoi(e) : 10;
+  }
+  return g_dq_variant;
+}
+int flash_attn_set_dq_variant(int v) {
+  const int old = dq_variant();
+  if (v >= 0) g_dq_variant = v;
+  return old;
+}
+constexpr size_t kMaxDsBytes = (size_t)16 << 30;  // dS buffer cap; above it dQ recomputes (variant 9)
+static size_t ds_bytes(int B, int S, int Hq) { return (size_t)B * Hq * S * S * 2; }
+static bool use_ds(int B, int S, int Hq) {
+  return dq_variant() == 10 && S % 256 == 0 && ds_bytes(B, S, Hq) <= kMaxDsBytes;
+}
+
 size_t flash_attn_bwd_workspace(int B, int S, int Hq, int D) {
-  // dk_part + dv_part (fp32, [B*S, Hq, D] each) + delta [B, Hq, S]
-  return (size_t)B * S * Hq * D * 4 * 2 + (size_t)B * Hq * S * 4;
+  // dk_part + dv_part (fp32, [B*S, Hq, D] each) + delta [B, Hq, S] (+ dS [B, Hq, S, S] bf16 for variant 10)
+  return (size_t)B * S * Hq * D * 4 * 2 + (size_t)B * Hq * S * 4 + (use_ds(B, S, Hq) ? ds_bytes(B, S, Hq) : 0);
 }
 
 template <int D>
@@ -633,22 +780,33 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
       o, dout, delta, B, S, Hq, os, dos);
   const size_t lds_kv = 32 * NW * (D * 2) + 2 * (2 * 32 * (D * 2) + 1024);
   const size_t lds_q = 4 * 64 * (D * 2);
+  const size_t lds_ds = 3 * (64 * (D * 2) + 256 * 64 * 2);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)fa_bwd_dkdv_kernel<D, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds_kv);
+    (void)hipFuncSetAttribute((const void*)fa_bwd_dkdv_kernel<D, NW, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv);
+    (void)hipFuncSetAttribute((const void*)fa_bwd_dkdv_kernel<D, NW, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv);
     (void)hipFuncSetAttribute((const void*)fa_bwd_dq_kernel<D, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds_q);
+    (void)hipFuncSetAttribute((const void*)fa_bwd_dq_ds_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds_ds);
     attr = true;
   }
-  fa_bwd_dkdv_kernel<D, NW><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(
-      q, k, v, dout, lse, delta, dk_part, dv_part, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);
-  static const int dq_variant = [] {
-    const char* e = getenv("KOP_DQ_VARIANT");
-    return e ? atoi(e) : 9;
-  }();
-  if (S % 256 == 0 && dq_variant >= 8) {
-    const bool stg = dq_variant == 9;
+  const int variant = dq_variant();
+  if (use_ds(B, S, Hq)) {
+    bf16_t* ds = reinterpret_cast<bf16_t*>(delta + (int64_t)B * Hq * S);
+    fa_bwd_dkdv_kernel<D, NW, true><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(
+        q, k, v, dout, lse, delta, dk_part, dv_part, ds, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);
+    fa_bwd_dq_ds_kernel<D><<<B * Hq * (S / 256), 512, lds_ds, stream>>>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale,
+                                                                        causal);
+    fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs);
+    return;
+  }
+  fa_bwd_dkdv_kernel<D, NW, false><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(
+      q, k, v, dout, lse, delta, dk_part, dv_part, nullptr, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);
+  if (S % 256 == 0 && variant >= 8) {
+    const bool stg = variant != 8;
     const size_t lds8 = (stg ? 4 : 3) * 2 * 64 * (D * 2);
     static bool attr8 = false;
     if (!attr8) {

@@ -44,6 +44,10 @@ int flash_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o,
                    int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, float scale, bool causal,
                    hipStream_t stream);
 size_t flash_attn_bwd_workspace(int B, int S, int Hq, int D);
+// dQ algorithm: 10 = from the materialised dS (default), 9 = recompute S/dP (8-wave, staggered),
+// 8 = lockstep, <8 = 4-wave.
+// v < 0 only queries; returns the previous value. The workspace size depends on it.
+int flash_attn_set_dq_variant(int v);
 int flash_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
                    const float* lse, bf16_t* dq, bf16_t* dk, bf16_t* dv, void* workspace, int B, int S, int Hq,
                    int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, int64_t dos, int64_t dqs,

@@ -283,3 +283,29 @@ def test_weight_grad_tn_layout_matches_nt():
     assert rel_err(out, ref) < 1e-2
     kf._dw_into(dy, x, out, True)
     assert rel_err(out, 2 * ref) < 1e-2
+
+
+@pytest.mark.parametrize("variant", [10, 9, 8])
+@pytest.mark.parametrize("D,Hq,Hkv,S", [(128, 8, 2, 512), (64, 4, 4, 256), (128, 4, 1, 768)])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_bwd_dq_variants(variant, D, Hq, Hkv, S, causal):
+    """every dQ algorithm (recompute 8/9, materialised dS 10) against the fp32 autograd reference."""
+    from kubeoperator_amd.ops.functional import rope_attention
+    from kubeoperator_amd.ops.reference import attention_ref
+
+    old = lib().flash_attn_set_dq_variant(variant)
+    try:
+        B = 2
+        torch.manual_seed(12)
+        qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+        o = rope_attention(qkv, None, None, B, S, Hq, Hkv, D, causal=causal, use_rope=False)
+        do = torch.randn_like(o)
+        (o.float() * do.float()).sum().backward()
+        x = qkv.detach().float().requires_grad_(True)
+        a, c = Hq * D, (Hq + Hkv) * D
+        of, _ = attention_ref(x[:, :a], x[:, a:c], x[:, c:], B, S, Hq, Hkv, D, causal)
+        (of * do.float()).sum().backward()
+        for lo, hi in ((0, a), (a, c), (c, x.shape[1])):
+            assert rel_err(qkv.grad[:, lo:hi], x.grad[:, lo:hi]) < 3e-2
+    finally:
+        lib().flash_attn_set_dq_variant(old)

@@ -149,17 +149,14 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
 #pragma unroll
   for (int i = 0; i < D / 32; ++i) dkacc[i] = dvacc[i] = f32x16{0};
 
+  // one barrier per stage: it publishes stage qt AND proves every wave is done with stage qt-1, whose slot
+  // the DMA of stage qt+1 then refills (prefetch distance: one stage of compute)
   for (int qt = qt0; qt < nqt; ++qt) {
     const int stage = (qt - qt0) & 1;
-    if (qt + 1 < nqt) {
-      issue(qt + 1, stage ^ 1);
-      if (wid == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MYP + 1) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MYP) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if (qt + 1 < nqt) issue(qt + 1, stage ^ 1);
     const char* Ql = smem + KB + stage * STAGE;
     const char* Ol = Ql + QT;
     const float* LD = reinterpret_cast<const float*>(Ql + 2 * QT);
@@ -214,6 +211,16 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
       }
       const bf16x8 pb[2] = {pack_acc8(sacc, 0), pack_acc8(sacc, 1)};
       const bf16x8 sb[2] = {pack_acc8(dpacc, 0), pack_acc8(dpacc, 1)};
+      if constexpr (WDS) {
+        // unscaled bf16 dS -> ds[b, hq, q, slot(key)]: per store the 32 keys of a row half-wave are 64
+        // contiguous bytes (the same rounding dK uses below);
+        // issued before the dK/dV products so their latency hides under them
+        // wave-uniform row pointer (SGPRs) + one 32-bit lane offset: no per-store 64-bit address VGPRs
+        const int loff = 4 * hh * S + ds_slot(key);
+        short* const dsw = reinterpret_cast<short*>(ds) + ((int64_t)(b * Hq + hq) * S + qs0) * S;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) dsw[(int64_t)((j & 3) + 8 * (j >> 2)) * S + loff] = sb[j >> 3][j & 7];
+      }
       // transposed dO / Q reads: rows 16s + 4hh + tq (+8) are tb_lane[(row0>>3)&1] + RB*(row0>>3), column
       // block dt is +512*dt (sub-tiled image, all immediates)
       const uint32_t o0 = lds_addr(Ol) + tb_lane0, o1 = lds_addr(Ol) + tb_lane1;
@@ -235,18 +242,8 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
           dkacc[dt] = mfma32(cat44(t[4 * s + 2], t[4 * s + 3]), sb[s], dkacc[dt]);
         }
       });
-      if constexpr (WDS) {
-        // unscaled bf16 dS -> ds[b, hq, q, slot(key)]: per store the 32 keys of a row half-wave are 64
-        // contiguous bytes (the same rounding dK uses below)
-        // wave-uniform row pointer (SGPRs) + one 32-bit lane offset: no per-store 64-bit address VGPRs
-        const int loff = 4 * hh * S + ds_slot(key);
-        short* const dsw = reinterpret_cast<short*>(ds) + ((int64_t)(b * Hq + hq) * S + qs0) * S;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) dsw[(int64_t)((j & 3) + 8 * (j >> 2)) * S + loff] = sb[j >> 3][j & 7];
-      }
     }
     asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // stage is refilled by the next iteration's DMA
   }
   // per-q-head partials: lane holds dK^T[d][key = k0w + r]
   float* dkp = dk_part + (int64_t)(b * S + k0w + r) * Hq * D + hq * D;
@@ -602,40 +599,52 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq8_kernel(
 
 // dQ from the materialised dS (KOP_DQ_VARIANT 10): dQ = scale * dS . K with dS written by the dK/dV kernel,
 // so neither S nor dP is recomputed (the recompute dQ kernels above redo 2 of their 3 MFMA products).
-// One workgroup = 8 waves = 256 queries of one (b, q-head), 64-key tiles: the K tile (read transposed, as
+// One workgroup = 8 waves = 256 query rows of HP q-heads sharing a KV head, 64-key tiles: the K tile (read transposed, as
 // the forward reads V) and the [256 x 64] dS tile both arrive by LDS-DMA into a 3-slot ring; per 16-key
 // group a lane's B fragment dS^T is one ds_read_b128 of its row (keys are stored in MFMA order, ds_slot),
 // and dQ^T += K^T . dS^T accumulates in DT independent chains. The dS stream (half of B*Hq*S*S bf16 under
 // a causal mask) makes this kernel HBM-bound, ~3x cheaper than recomputing.
-template <int D>
+template <int D, int HP>
 __global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __restrict__ ds, const bf16_t* __restrict__ k,
                                                               bf16_t* __restrict__ dq, int B, int S, int Hq, int Hkv,
                                                               int64_t ks, int64_t dqs, float scale, int causal) {
-  constexpr int NW = 8, BM = 256, BN = 64, ROWB = D * 2, NSLOT = 3;
+  // HP q-heads of one GQA group per workgroup (RH = 256/HP query rows each) share every K tile: the
+  // kernel streams dS, so K re-reads from L2/MALL are the traffic worth cutting
+  constexpr int NW = 8, BM = 256, RH = BM / HP, WPH = NW / HP, BN = 64, ROWB = D * 2, NSLOT = 3;
   constexpr int KT = BN * ROWB, DST = BM * BN * 2, SLOT = KT + DST;
   constexpr int PPW = (KT / 1024) / NW + (DST / 1024) / NW;  // DMA pieces per wave per tile
   static_assert((KT / 1024) % NW == 0 && (DST / 1024) % NW == 0, "tiles must split evenly over the waves");
+  static_assert(RH % 32 == 0, "each wave owns 32 rows of one head");
   constexpr int DT = D / 32, NR = 2 * DT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5;
   const int tq = (lane & 15) >> 2, tp = lane & 3, tg1 = (lane >> 4) & 1;
-  const int nqb = S / BM;
-  const int nwork = B * Hq * nqb;
+  const int ngrp = Hq / HP, nqb = S / RH;
+  const int nwork = B * ngrp * nqb;
   const int work = xcd_remap(blockIdx.x, nwork);
-  const int qb = causal ? (nqb - 1 - work / (B * Hq)) : work / (B * Hq);
-  const int rest = work % (B * Hq);
-  const int b = rest / Hq, hq = rest % Hq;
-  const int kvh = hq / (Hq / Hkv);
-  const int q0 = qb * BM, q0w = q0 + wid * 32;
-  const int ntiles = causal ? (q0 + BM) / BN : S / BN;
+  const int qb = causal ? (nqb - 1 - work / (B * ngrp)) : work / (B * ngrp);
+  const int rest = work % (B * ngrp);
+  const int b = rest / ngrp, hg = rest % ngrp;
+  const int kvh = (hg * HP) / (Hq / Hkv);
+  const int hq = hg * HP + wid / WPH;  // this wave's head
+  const int q0 = qb * RH, q0w = q0 + 32 * (wid % WPH);
+  const int ntiles = causal ? (q0 + RH + BN - 1) / BN : S / BN;
   const bf16_t* kbase = k + (int64_t)(b * S) * ks + kvh * D;
-  const bf16_t* dsbase = ds + ((int64_t)(b * Hq + hq) * S + q0) * S;
+  // dS tile: rows 0..255 of the image = HP heads x RH rows; an 8-row DMA piece never straddles heads
+  const int lrow = (lane & 31) >> 2, lhi = lane >> 5, lslot = lane & 3;
   auto issue = [&](int t) {
     char* sl = smem + (t % NSLOT) * SLOT;
     dma_tile_a<ROWB, NW, BN>(sl, kbase + (int64_t)(t * BN) * ks, ks, wid, lane);
-    dma_tile_a<BN * 2, NW, BM>(sl + KT, dsbase + t * BN, S, wid, lane);
+#pragma unroll
+    for (int i = 0; i < (DST / 1024) / NW; ++i) {
+      const int piece = wid + i * NW;
+      const int row = 8 * piece + lrow;
+      const int ch = 4 * lhi + (lslot ^ ((row >> 2) & 3));
+      const bf16_t* src = ds + ((int64_t)(b * Hq + hg * HP + row / RH) * S + q0 + row % RH) * S + t * BN + ch * 8;
+      glds16(src, sl + KT + piece * 1024);
+    }
   };
   issue(0);
   if (ntiles > 1) issue(1);
@@ -644,7 +653,7 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __re
   // K^T transposed reads (as the forward's V^T): rows R0 + 4hh + tq (+8) at column block dt
   const int kb_lane0 = 64 * (4 * hh + tq) + 16 * ((2 * tg1 + (tp >> 1)) ^ hh) + 8 * (tp & 1);
   const int kb_lane1 = 64 * (4 * hh + tq) + 16 * ((2 * tg1 + (tp >> 1)) ^ (2 + hh)) + 8 * (tp & 1);
-  // dS row reads of row 32*wid + r at chunk 2*ks4 + hh in the sub-tiled [256][128 B] image
+  // dS row reads of image row 32*wid + r at chunk 2*ks4 + hh in the sub-tiled [256][128 B] image
   const int ds_lane0 = 4096 * wid + 1024 * (r >> 3) + 64 * (r & 7) + 16 * (hh ^ ((r >> 2) & 3));
   const int ds_lane1 = 4096 * wid + 1024 * (r >> 3) + 64 * (r & 7) + 16 * ((2 + hh) ^ ((r >> 2) & 3));
   f32x16 acc[DT];
@@ -693,7 +702,6 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __re
     }
     asm volatile("" ::: "memory");
   }
-  __builtin_amdgcn_s_barrier();
   bf16_t* dp = dq + (int64_t)(b * S + qi) * dqs + hq * D;
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) {
@@ -705,6 +713,20 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __re
       *reinterpret_cast<u32x2*>(dp + dt * 32 + 8 * g4 + 4 * hh) = w;
     }
   }
+}
+
+template <int D, int HP>
+static void launch_dq_ds(const bf16_t* ds, const bf16_t* k, bf16_t* dq, int B, int S, int Hq, int Hkv, int64_t ks,
+                         int64_t dqs, float scale, bool causal, hipStream_t stream) {
+  const size_t lds = 3 * (64 * (D * 2) + 256 * 64 * 2);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)fa_bwd_dq_ds_kernel<D, HP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    attr = true;
+  }
+  fa_bwd_dq_ds_kernel<D, HP><<<B * (Hq / HP) * (S / (256 / HP)), 512, lds, stream>>>(ds, k, dq, B, S, Hq, Hkv, ks,
+                                                                                    dqs, scale, causal);
 }
 
 // dk/dv = bf16(sum over the GQA group of the per-q-head partials)
@@ -780,7 +802,6 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
       o, dout, delta, B, S, Hq, os, dos);
   const size_t lds_kv = 32 * NW * (D * 2) + 2 * (2 * 32 * (D * 2) + 1024);
   const size_t lds_q = 4 * 64 * (D * 2);
-  const size_t lds_ds = 3 * (64 * (D * 2) + 256 * 64 * 2);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)fa_bwd_dkdv_kernel<D, NW, false>,
@@ -789,8 +810,6 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv);
     (void)hipFuncSetAttribute((const void*)fa_bwd_dq_kernel<D, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds_q);
-    (void)hipFuncSetAttribute((const void*)fa_bwd_dq_ds_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds_ds);
     attr = true;
   }
   const int variant = dq_variant();
@@ -798,8 +817,12 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
     bf16_t* ds = reinterpret_cast<bf16_t*>(delta + (int64_t)B * Hq * S);
     fa_bwd_dkdv_kernel<D, NW, true><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(
         q, k, v, dout, lse, delta, dk_part, dv_part, ds, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);
-    fa_bwd_dq_ds_kernel<D><<<B * Hq * (S / 256), 512, lds_ds, stream>>>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale,
-                                                                        causal);
+    const int grp = Hq / Hkv;  // heads per workgroup: largest power of two dividing the GQA group, <= 8
+    const int hp = (grp % 8 == 0) ? 8 : (grp % 4 == 0) ? 4 : (grp % 2 == 0) ? 2 : 1;
+    if (hp == 8) launch_dq_ds<D, 8>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+    else if (hp == 4) launch_dq_ds<D, 4>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+    else if (hp == 2) launch_dq_ds<D, 2>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+    else launch_dq_ds<D, 1>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
     fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs);
     return;
   }

@@ -286,7 +286,7 @@ def test_weight_grad_tn_layout_matches_nt():
 
 
 @pytest.mark.parametrize("variant", [10, 9, 8])
-@pytest.mark.parametrize("D,Hq,Hkv,S", [(128, 8, 2, 512), (64, 4, 4, 256), (128, 4, 1, 768)])
+@pytest.mark.parametrize("D,Hq,Hkv,S", [(128, 8, 2, 512), (64, 4, 4, 256), (128, 4, 1, 768), (128, 8, 1, 256), (64, 8, 4, 512)])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_attention_bwd_dq_variants(variant, D, Hq, Hkv, S, causal):
     """every dQ algorithm (recompute 8/9, materialised dS 10) against the fp32 autograd reference."""

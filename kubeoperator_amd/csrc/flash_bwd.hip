@@ -34,9 +34,13 @@
 namespace kop {
 
 // delta[b, h, s] = sum_d dO * O
+// and the dK/dV kernel's accumulator initialisers: nlse = -lse / scale (S = Q.K^T starts there, so
+// p = exp2(c * acc)) and ndelta = -delta (dP starts there) -- no negate / scale VALU per stage
 template <int D>
 __global__ void __launch_bounds__(256) fa_bwd_delta_kernel(const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout,
-                                                           float* __restrict__ delta, int B, int S, int Hq, int64_t os,
+                                                           const float* __restrict__ lse, float* __restrict__ delta,
+                                                           float* __restrict__ nlse, float* __restrict__ ndelta,
+                                                           float lse_mul, int B, int S, int Hq, int64_t os,
                                                            int64_t dos) {
   constexpr int LPR = D / 8;  // lanes per row
   const int64_t rows = (int64_t)B * S * Hq;
@@ -58,7 +62,10 @@ __global__ void __launch_bounds__(256) fa_bwd_delta_kernel(const bf16_t* __restr
     const int64_t t = row / Hq;
     const int h = (int)(row % Hq);
     const int bb = (int)(t / S), s = (int)(t % S);
-    delta[((int64_t)(bb * Hq + h)) * S + s] = a;
+    const int64_t i = ((int64_t)(bb * Hq + h)) * S + s;
+    delta[i] = a;
+    ndelta[i] = -a;
+    nlse[i] = -lse[i] * lse_mul;
   }
 }
 
@@ -74,7 +81,7 @@ __device__ __forceinline__ int ds_slot(int key) {
 template <int D, int NW, bool WDS = false>
 __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
-    const bf16_t* __restrict__ dout, const float* __restrict__ lse, const float* __restrict__ delta,
+    const bf16_t* __restrict__ dout, const float* __restrict__ nlse, const float* __restrict__ ndelta,
     float* __restrict__ dk_part, float* __restrict__ dv_part, bf16_t* __restrict__ ds, int B, int S, int Hq,
     int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t dos, float scale, int causal) {
   // LDS: the workgroup's K block (BN rows, read as the S = Q.K^T B operand) + a 2-deep ring of 32-query
@@ -100,10 +107,9 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
   const int kvh = hq / (Hq / Hkv);
   const int k0 = kb * BN, k0w = k0 + 32 * wid;
   const float c2 = scale * 1.4426950408889634f;
-  const float lse_mul = 1.f / scale;
 
-  const float* lse_h = lse + ((int64_t)(b * Hq + hq)) * S;
-  const float* del_h = delta + ((int64_t)(b * Hq + hq)) * S;
+  const float* lse_h = nlse + ((int64_t)(b * Hq + hq)) * S;
+  const float* del_h = ndelta + ((int64_t)(b * Hq + hq)) * S;
   const bf16_t* qbase = q + (int64_t)(b * S) * qs + hq * D;
   const bf16_t* dobase = dout + (int64_t)(b * S) * dos + hq * D;
   // first query tile that sees any key of this workgroup; the waves of later keys skip leading tiles
@@ -170,8 +176,8 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
         const f32x4 dv = *reinterpret_cast<const f32x4*>(LD + 32 + qr);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          sacc[4 * g4 + e] = -lv[e] * lse_mul;
-          dpacc[4 * g4 + e] = -dv[e];
+          sacc[4 * g4 + e] = lv[e];
+          dpacc[4 * g4 + e] = dv[e];
         }
       }
       (void)raddr;
@@ -201,11 +207,12 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
         });
       }
       const int key = k0w + r;
+      // key > query  <=>  kd > (j & 3) + 8 * (j >> 2): one subtraction, then compares with constants
+      const int kd = causal ? key - qs0 - 4 * hh : -1;
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
-        const int qi = qs0 + (j & 3) + 8 * (j >> 2) + 4 * hh;
         float p = __builtin_amdgcn_exp2f(sacc[j] * c2);
-        if (causal && key > qi) p = 0.f;
+        if (kd > (j & 3) + 8 * (j >> 2)) p = 0.f;
         sacc[j] = p;
         dpacc[j] = p * dpacc[j];
       }
@@ -216,10 +223,19 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
         // contiguous bytes (the same rounding dK uses below);
         // issued before the dK/dV products so their latency hides under them
         // wave-uniform row pointer (SGPRs) + one 32-bit lane offset: no per-store 64-bit address VGPRs
-        const int loff = 4 * hh * S + ds_slot(key);
-        short* const dsw = reinterpret_cast<short*>(ds) + ((int64_t)(b * Hq + hq) * S + qs0) * S;
+        // saddr stores: 64-bit row pointer in SGPRs (SALU adds), 32-bit lane byte offset in one VGPR; the
+        // loop-top vmcnt(0) retires them (hipcc does not see these stores)
+        const uint32_t loff = 2u * (uint32_t)(4 * hh * S + ds_slot(key));
+        const uint64_t row0 = (uint64_t)(uintptr_t)(ds + ((int64_t)(b * Hq + hq) * S + qs0) * S);
+        const u32x4 w0 = __builtin_bit_cast(u32x4, sb[0]), w1 = __builtin_bit_cast(u32x4, sb[1]);
 #pragma unroll
-        for (int j = 0; j < 16; ++j) dsw[(int64_t)((j & 3) + 8 * (j >> 2)) * S + loff] = sb[j >> 3][j & 7];
+        for (int j = 0; j < 16; j += 2) {
+          const uint32_t w = (j < 8) ? w0[j >> 1] : w1[(j - 8) >> 1];
+          const uint64_t ra = row0 + (uint64_t)(2 * ((j & 3) + 8 * (j >> 2))) * (uint64_t)S;
+          const uint64_t rb = ra + 2ull * (uint64_t)S;
+          asm volatile("global_store_short %0, %1, %2" ::"v"(loff), "v"(w), "s"(ra) : "memory");
+          asm volatile("global_store_short_d16_hi %0, %1, %2" ::"v"(loff), "v"(w), "s"(rb) : "memory");
+        }
       }
       // transposed dO / Q reads: rows 16s + 4hh + tq (+8) are tb_lane[(row0>>3)&1] + RB*(row0>>3), column
       // block dt is +512*dt (sub-tiled image, all immediates)
@@ -783,8 +799,9 @@ static bool use_ds(int B, int S, int Hq) {
 }
 
 size_t flash_attn_bwd_workspace(int B, int S, int Hq, int D) {
-  // dk_part + dv_part (fp32, [B*S, Hq, D] each) + delta [B, Hq, S] (+ dS [B, Hq, S, S] bf16 for variant 10)
-  return (size_t)B * S * Hq * D * 4 * 2 + (size_t)B * Hq * S * 4 + (use_ds(B, S, Hq) ? ds_bytes(B, S, Hq) : 0);
+  // dk_part + dv_part (fp32, [B*S, Hq, D] each) + delta, nlse, ndelta ([B, Hq, S] each)
+  // (+ dS [B, Hq, S, S] bf16 for variant 10)
+  return (size_t)B * S * Hq * D * 4 * 2 + (size_t)B * Hq * S * 4 * 3 + (use_ds(B, S, Hq) ? ds_bytes(B, S, Hq) : 0);
 }
 
 template <int D>
@@ -797,9 +814,11 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
   float* dk_part = reinterpret_cast<float*>(workspace);
   float* dv_part = dk_part + T * Hq * D;
   float* delta = dv_part + T * Hq * D;
+  float* nlse = delta + T * Hq;
+  float* ndelta = nlse + T * Hq;
   const int rows_per_block = 256 / (D / 8);
   fa_bwd_delta_kernel<D><<<(int)((T * Hq + rows_per_block - 1) / rows_per_block), 256, 0, stream>>>(
-      o, dout, delta, B, S, Hq, os, dos);
+      o, dout, lse, delta, nlse, ndelta, 1.f / scale, B, S, Hq, os, dos);
   const size_t lds_kv = 32 * NW * (D * 2) + 2 * (2 * 32 * (D * 2) + 1024);
   const size_t lds_q = 4 * 64 * (D * 2);
   static bool attr = false;
@@ -814,9 +833,9 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
   }
   const int variant = dq_variant();
   if (use_ds(B, S, Hq)) {
-    bf16_t* ds = reinterpret_cast<bf16_t*>(delta + (int64_t)B * Hq * S);
+    bf16_t* ds = reinterpret_cast<bf16_t*>(ndelta + T * Hq);
     fa_bwd_dkdv_kernel<D, NW, true><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(
-        q, k, v, dout, lse, delta, dk_part, dv_part, ds, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);
+        q, k, v, dout, nlse, ndelta, dk_part, dv_part, ds, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);
     const int grp = Hq / Hkv;  // heads per workgroup: largest power of two dividing the GQA group, <= 8
     const int hp = (grp % 8 == 0) ? 8 : (grp % 4 == 0) ? 4 : (grp % 2 == 0) ? 2 : 1;
     if (hp == 8) launch_dq_ds<D, 8>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
@@ -827,7 +846,7 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
     return;
   }
   fa_bwd_dkdv_kernel<D, NW, false><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(
-      q, k, v, dout, lse, delta, dk_part, dv_part, nullptr, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);
+      q, k, v, dout, nlse, ndelta, dk_part, dv_part, nullptr, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);
   if (S % 256 == 0 && variant >= 8) {
     const bool stg = variant != 8;
     const size_t lds8 = (stg ? 4 : 3) * 2 * 64 * (D * 2);

@@ -22,7 +22,6 @@ stream; ``ProcessGroupNCCL`` orders them after the producing GEMMs on the comput
 """
 from __future__ import annotations
 
-import torch
 import torch.distributed as dist
 
 from ..ops.optim import Segment
@@ -44,7 +43,6 @@ class DataParallel:
         self._gather_works = []
         self.comm_bytes = 0
         store.on_ready = self._on_ready
-        self._nccl = info.backend == "nccl"
         self.overlapped = False  # set once the optimizer publishes ZeRO-1 gathers itself
 
     # -------------------------------------------------------------------------------------------
@@ -57,7 +55,7 @@ class DataParallel:
             return
         g = self.store.grads[b.start:b.end]
         self.comm_bytes += g.numel() * g.element_size()
-        if self.mode == "allreduce" or not self._nccl:
+        if self.mode == "allreduce":
             self._works.append(dist.all_reduce(g, async_op=True))
         else:
             a, e = b.piece(self.rank, self.world)
@@ -93,17 +91,9 @@ class DataParallel:
         return self._gather(b, a, e, async_op=True)
 
     def _gather(self, b: Bucket, a: int, e: int, async_op: bool):
+        """In-place all-gather of the bucket's updated pieces (RCCL on GPU; gloo runs the same call on CPU)."""
         st = self.store
-        full = st.params[b.start:b.end]
-        if self._nccl:
-            return dist.all_gather_into_tensor(full, st.params[a:e], async_op=async_op)
-        n = e - a
-        outs = [full[i * n:(i + 1) * n] for i in range(self.world)]
-        tmp = [torch.empty_like(o) for o in outs]
-        dist.all_gather(tmp, st.params[a:e].clone())
-        for o, t in zip(outs, tmp):
-            o.copy_(t)
-        return None
+        return dist.all_gather_into_tensor(st.params[b.start:b.end], st.params[a:e], async_op=async_op)
 
     def norm_allreduce(self):
         if self.mode == "zero1" and self.world > 1:
@@ -117,7 +107,7 @@ class DataParallel:
         st = self.store
         for b in st.buckets:
             a, e = b.piece(self.rank, self.world)
-            w = self._gather(b, a, e, async_op=self._nccl)
+            w = self._gather(b, a, e, async_op=True)
             if w is not None:
                 self._gather_works.append(w)
         self.wait_params()

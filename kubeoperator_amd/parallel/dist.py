@@ -42,6 +42,9 @@ def init_distributed(device: str = "auto", timeout_s: int = 1800) -> DistInfo:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         kw = {}
+        init = os.environ.get("KOP_DIST_INIT")  # e.g. file:///tmp/x (tests: no TCP port race)
+        if init:
+            kw["init_method"] = init
         if use_gpu:
             kw["device_id"] = dev
         dist.init_process_group(backend=backend, rank=rank, world_size=world,

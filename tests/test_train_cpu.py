@@ -2,7 +2,6 @@
 flat bucketed store + fused AdamW against torch.optim.AdamW, DDP all-reduce and ZeRO-1 over gloo with
 world size 2 matching a single process on the global batch, and checkpoint resume being bit-identical."""
 import os
-import socket
 
 import pytest
 import torch
@@ -59,45 +58,44 @@ def test_fused_adamw_matches_torch():
     torch.testing.assert_close(p.float(), ref.detach(), atol=1e-2, rtol=1e-2)
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+def _unpadded(tr):
+    """Parameters in layout order without bucket padding (the padding depends on the world size)."""
+    return torch.cat([p.detach().reshape(-1).float() for _, p in tr.store.named_params()])
 
 
-def _ddp_worker(rank, world, port, mode, out_q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
+def _ddp_worker(rank, world, init, mode, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      KOP_DIST_INIT=init)
     torch.set_num_threads(1)
     from kubeoperator_amd.parallel.dist import init_distributed, shutdown
     info = init_distributed("cpu")
     tr = Trainer(_tc(micro_batch=2, dp_mode=mode), info)
     for step in range(3):
-        ids, tgt = _batch(tr, seed=step, mb=4)
+        ids, tgt = _batch(tr, seed=step, mb=2 * world)
         tr.train_step([(ids[2 * rank:2 * rank + 2], tgt[2 * rank:2 * rank + 2])])
     if rank == 0:
-        out_q.put(tr.store.params.float().clone())
+        out_q.put(_unpadded(tr).numpy())  # by value: a shared-memory tensor dies with this process
     shutdown(info)
 
 
-@pytest.mark.parametrize("mode", ["allreduce", "zero1"])
-def test_data_parallel_gloo_matches_single_process(mode):
+@pytest.mark.parametrize("mode,world", [("allreduce", 2), ("zero1", 2), ("zero1", 4)])
+def test_data_parallel_gloo_matches_single_process(mode, world, tmp_path):
+    """The exact collective calls of the RCCL path (in-place reduce_scatter_tensor / all_gather_into_tensor,
+    async all_reduce) run over gloo here; the result must equal one process on the global batch."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    init = f"file://{tmp_path}/rendezvous"  # file store: no free-port race between parallel test workers
+    procs = [ctx.Process(target=_ddp_worker, args=(r, world, init, mode, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=300)
+    got = torch.from_numpy(q.get(timeout=300))
     for p in procs:
         p.join(120)
         assert p.exitcode == 0
-    single = Trainer(_tc(micro_batch=4), DistInfo())
+    single = Trainer(_tc(micro_batch=2 * world), DistInfo())
     for step in range(3):
-        single.train_step([_batch(single, seed=step, mb=4)])
-    torch.testing.assert_close(got, single.store.params.float(), atol=2e-2, rtol=0)
+        single.train_step([_batch(single, seed=step, mb=2 * world)])
+    torch.testing.assert_close(got, _unpadded(single), atol=2e-2, rtol=0)
 
 
 def test_checkpoint_resume_is_exact(tmp_path):

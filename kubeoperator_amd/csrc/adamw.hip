@@ -15,6 +15,9 @@
 
 namespace kop {
 
+// Every byte is touched exactly once per step. Plain (cached) loads and stores: non-temporal ones measured
+// 1 % slower on the whole training step (the update overlaps the next forward). The update uses the
+// hardware sqrt / reciprocal.
 __global__ void __launch_bounds__(256) adamw_kernel(bf16_t* __restrict__ p, const bf16_t* __restrict__ g,
                                                     float* __restrict__ master, float* __restrict__ m,
                                                     float* __restrict__ v, int64_t n8, float lr, float b1, float b2,
@@ -22,31 +25,30 @@ __global__ void __launch_bounds__(256) adamw_kernel(bf16_t* __restrict__ p, cons
                                                     float gscale, const float* __restrict__ gscale_dev) {
   const float gs = gscale * (gscale_dev ? gscale_dev[0] : 1.f);
   const float decay = 1.f - lr * wd;
+  const float step = lr * inv_bc1;
   for (int64_t it = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; it < n8; it += (int64_t)gridDim.x * blockDim.x) {
-    float gf[8];
-    unpack8(reinterpret_cast<const u32x4*>(g)[it], gf);
     f32x4* mp = reinterpret_cast<f32x4*>(master) + it * 2;
     f32x4* mm = reinterpret_cast<f32x4*>(m) + it * 2;
     f32x4* vv = reinterpret_cast<f32x4*>(v) + it * 2;
-    float w[8], mv[8], vv8[8];
-    {
-      const f32x4 w0 = mp[0], w1 = mp[1], m0 = mm[0], m1 = mm[1], v0 = vv[0], v1 = vv[1];
+    const u32x4 graw = reinterpret_cast<const u32x4*>(g)[it];
+    const f32x4 w0 = mp[0], w1 = mp[1];
+    const f32x4 m0 = mm[0], m1 = mm[1];
+    const f32x4 v0 = vv[0], v1 = vv[1];
+    float gf[8], w[8], mv[8], vv8[8];
+    unpack8(graw, gf);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        w[i] = w0[i]; w[i + 4] = w1[i];
-        mv[i] = m0[i]; mv[i + 4] = m1[i];
-        vv8[i] = v0[i]; vv8[i + 4] = v1[i];
-      }
+    for (int i = 0; i < 4; ++i) {
+      w[i] = w0[i]; w[i + 4] = w1[i];
+      mv[i] = m0[i]; mv[i + 4] = m1[i];
+      vv8[i] = v0[i]; vv8[i + 4] = v1[i];
     }
-    float out[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float gi = gf[i] * gs;
       mv[i] = b1 * mv[i] + (1.f - b1) * gi;
       vv8[i] = b2 * vv8[i] + (1.f - b2) * gi * gi;
-      const float denom = sqrtf(vv8[i]) * inv_sqrt_bc2 + eps;
-      w[i] = w[i] * decay - lr * (mv[i] * inv_bc1) / denom;
-      out[i] = w[i];
+      const float denom = __builtin_amdgcn_sqrtf(vv8[i]) * inv_sqrt_bc2 + eps;
+      w[i] = w[i] * decay - step * mv[i] * __builtin_amdgcn_rcpf(denom);
     }
     mp[0] = f32x4{w[0], w[1], w[2], w[3]};
     mp[1] = f32x4{w[4], w[5], w[6], w[7]};
@@ -54,7 +56,7 @@ __global__ void __launch_bounds__(256) adamw_kernel(bf16_t* __restrict__ p, cons
     mm[1] = f32x4{mv[4], mv[5], mv[6], mv[7]};
     vv[0] = f32x4{vv8[0], vv8[1], vv8[2], vv8[3]};
     vv[1] = f32x4{vv8[4], vv8[5], vv8[6], vv8[7]};
-    reinterpret_cast<u32x4*>(p)[it] = pack8(out);
+    reinterpret_cast<u32x4*>(p)[it] = pack8(w);
   }
 }
 

@@ -15,51 +15,50 @@ namespace kop {
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) rope_kernel(bf16_t* __restrict__ x, const float* __restrict__ cos_t,
                                                    const float* __restrict__ sin_t, const int* __restrict__ pos,
-                                                   int64_t T, int S, int nheads, int D, int64_t row_stride,
-                                                   float sign) {
+                                                   int S, int nheads, int D, int64_t row_stride, float sign) {
+  // grid: (T, ceil(items_per_token / 256)); item = (head, group of 8 rotary pairs) of token blockIdx.x
   const int half = D >> 1;
-  const int per_head = half >> 3;  // work items per head
-  const int64_t total = T * nheads * per_head;
-  for (int it = blockIdx.x * blockDim.x + threadIdx.x; it < (int)total; it += gridDim.x * blockDim.x) {
-    const int j = (int)(it % per_head);
-    const int th = it / per_head;
-    const int h = (int)(th % nheads);
-    const int64_t t = th / nheads;
-    const int p = pos ? pos[t] : (int)(t % S);
-    bf16_t* base = x + t * row_stride + (int64_t)h * D + j * 8;
-    u32x4* lo = reinterpret_cast<u32x4*>(base);
-    u32x4* hi = reinterpret_cast<u32x4*>(base + half);
-    const f32x4* cp = reinterpret_cast<const f32x4*>(cos_t + (int64_t)p * half + j * 8);
-    const f32x4* sp = reinterpret_cast<const f32x4*>(sin_t + (int64_t)p * half + j * 8);
-    float a[8], b[8], c[8], s[8];
-    unpack8(*lo, a);
-    unpack8(*hi, b);
-    f32x4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
+  const int per_head = half >> 3;
+  const int item = blockIdx.y * blockDim.x + threadIdx.x;
+  if (item >= nheads * per_head) return;
+  const int64_t t = blockIdx.x;
+  const int h = item / per_head, j = item - h * per_head;
+  const int p = pos ? pos[t] : (int)(t % S);
+  bf16_t* base = x + t * row_stride + (int64_t)h * D + j * 8;
+  u32x4* lo = reinterpret_cast<u32x4*>(base);
+  u32x4* hi = reinterpret_cast<u32x4*>(base + half);
+  const f32x4* cp = reinterpret_cast<const f32x4*>(cos_t + (int64_t)p * half + j * 8);
+  const f32x4* sp = reinterpret_cast<const f32x4*>(sin_t + (int64_t)p * half + j * 8);
+  const u32x4 lv = *lo, hv = *hi;
+  const f32x4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
+  float a[8], b[8], c[8], sn[8];
+  unpack8(lv, a);
+  unpack8(hv, b);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      c[i] = c0[i];
-      c[i + 4] = c1[i];
-      s[i] = s0[i] * sign;
-      s[i + 4] = s1[i] * sign;
-    }
-    float o1[8], o2[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      o1[i] = a[i] * c[i] - b[i] * s[i];
-      o2[i] = b[i] * c[i] + a[i] * s[i];
-    }
-    *lo = pack8(o1);
-    *hi = pack8(o2);
+  for (int i = 0; i < 4; ++i) {
+    c[i] = c0[i];
+    c[i + 4] = c1[i];
+    sn[i] = s0[i] * sign;
+    sn[i + 4] = s1[i] * sign;
   }
+  float o1[8], o2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    o1[i] = a[i] * c[i] - b[i] * sn[i];
+    o2[i] = b[i] * c[i] + a[i] * sn[i];
+  }
+  *lo = pack8(o1);
+  *hi = pack8(o2);
 }
 
 int rope_inplace(bf16_t* x, const float* cos_t, const float* sin_t, const int* pos, int64_t T, int S, int nheads,
                  int D, int64_t row_stride, bool inverse, hipStream_t stream) {
   if (D % 16 != 0 || row_stride % 8 != 0) return -1;
-  if (T * nheads * (D / 16) >= (1ll << 31)) return -3;
-  const int64_t total = T * nheads * (D / 16);
-  rope_kernel<<<stream_grid(total, 256), 256, 0, stream>>>(x, cos_t, sin_t, pos, T, S, nheads, D, row_stride,
-                                                           inverse ? -1.f : 1.f);
+  if (T == 0) return 0;
+  if (T >= (1ll << 31)) return -3;
+  const int items = nheads * (D / 16);
+  const dim3 grid((unsigned)T, (items + 255) / 256);
+  rope_kernel<<<grid, 256, 0, stream>>>(x, cos_t, sin_t, pos, S, nheads, D, row_stride, inverse ? -1.f : 1.f);
   return 0;
 }
 
@@ -68,58 +67,64 @@ int rope_inplace(bf16_t* x, const float* cos_t, const float* sin_t, const int* p
 //   fwd: h = silu(gate) * up                  [T, F]
 //   bwd: dgate = dh * up * sig * (1 + gate*(1-sig)),  dup = dh * silu(gate)  -> dgu [T, 2F]
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) swiglu_fwd_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ h,
-                                                         int64_t T, int F) {
-  const int cpr = F >> 3;
-  const int64_t total = T * cpr;
-  for (int it = blockIdx.x * blockDim.x + threadIdx.x; it < (int)total; it += gridDim.x * blockDim.x) {
-    const int64_t t = it / cpr;
-    const int c = (int)(it % cpr);
-    const bf16_t* row = gu + t * 2 * F;
-    float g[8], u[8], o[8];
-    unpack8(reinterpret_cast<const u32x4*>(row)[c], g);
-    unpack8(reinterpret_cast<const u32x4*>(row + F)[c], u);
+// grid: (T, ceil(F/8 / 256)): one 16-byte chunk of gate and up per thread, no grid-stride loop and no
+// per-item integer division; sigmoid through the hardware reciprocal (v_rcp_f32, 1 ulp)
+__device__ __forceinline__ float sigmoidf_fast(float g) { return __builtin_amdgcn_rcpf(1.f + __expf(-g)); }
+
+__global__ void __launch_bounds__(256) swiglu_fwd_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ h, int F) {
+  const int c = blockIdx.y * blockDim.x + threadIdx.x;
+  if (c >= (F >> 3)) return;
+  const int64_t t = blockIdx.x;
+  const bf16_t* row = gu + t * 2 * F;
+  const u32x4 gv = reinterpret_cast<const u32x4*>(row)[c];
+  const u32x4 uv = reinterpret_cast<const u32x4*>(row + F)[c];
+  float g[8], u[8], o[8];
+  unpack8(gv, g);
+  unpack8(uv, u);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = g[i] / (1.f + __expf(-g[i])) * u[i];
-    reinterpret_cast<u32x4*>(h + t * F)[c] = pack8(o);
-  }
+  for (int i = 0; i < 8; ++i) o[i] = g[i] * sigmoidf_fast(g[i]) * u[i];
+  reinterpret_cast<u32x4*>(h + t * F)[c] = pack8(o);
 }
 
 __global__ void __launch_bounds__(256) swiglu_bwd_kernel(const bf16_t* __restrict__ gu, const bf16_t* __restrict__ dh,
-                                                         bf16_t* __restrict__ dgu, int64_t T, int F) {
-  const int cpr = F >> 3;
-  const int64_t total = T * cpr;
-  for (int it = blockIdx.x * blockDim.x + threadIdx.x; it < (int)total; it += gridDim.x * blockDim.x) {
-    const int64_t t = it / cpr;
-    const int c = (int)(it % cpr);
-    const bf16_t* row = gu + t * 2 * F;
-    float g[8], u[8], d[8], dg[8], du[8];
-    unpack8(reinterpret_cast<const u32x4*>(row)[c], g);
-    unpack8(reinterpret_cast<const u32x4*>(row + F)[c], u);
-    unpack8(reinterpret_cast<const u32x4*>(dh + t * F)[c], d);
+                                                         bf16_t* __restrict__ dgu, int F) {
+  const int c = blockIdx.y * blockDim.x + threadIdx.x;
+  if (c >= (F >> 3)) return;
+  const int64_t t = blockIdx.x;
+  const bf16_t* row = gu + t * 2 * F;
+  const u32x4 gv = reinterpret_cast<const u32x4*>(row)[c];
+  const u32x4 uv = reinterpret_cast<const u32x4*>(row + F)[c];
+  const u32x4 dv = reinterpret_cast<const u32x4*>(dh + t * F)[c];
+  float g[8], u[8], d[8], dg[8], du[8];
+  unpack8(gv, g);
+  unpack8(uv, u);
+  unpack8(dv, d);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float sg = 1.f / (1.f + __expf(-g[i]));
-      const float silu = g[i] * sg;
-      du[i] = d[i] * silu;
-      dg[i] = d[i] * u[i] * sg * (1.f + g[i] * (1.f - sg));
-    }
-    bf16_t* orow = dgu + t * 2 * F;
-    reinterpret_cast<u32x4*>(orow)[c] = pack8(dg);
-    reinterpret_cast<u32x4*>(orow + F)[c] = pack8(du);
+  for (int i = 0; i < 8; ++i) {
+    const float sg = sigmoidf_fast(g[i]);
+    const float silu = g[i] * sg;
+    du[i] = d[i] * silu;
+    dg[i] = d[i] * u[i] * sg * (1.f + g[i] * (1.f - sg));
   }
+  bf16_t* orow = dgu + t * 2 * F;
+  reinterpret_cast<u32x4*>(orow)[c] = pack8(dg);
+  reinterpret_cast<u32x4*>(orow + F)[c] = pack8(du);
 }
 
 int swiglu_fwd(const bf16_t* gu, bf16_t* h, int64_t T, int F, hipStream_t stream) {
   if (F % 8) return -1;
-  if (T * (F / 8) >= (1ll << 31)) return -3;
-  swiglu_fwd_kernel<<<stream_grid(T * (F / 8), 256), 256, 0, stream>>>(gu, h, T, F);
+  if (T == 0) return 0;
+  if (T >= (1ll << 31)) return -3;
+  const dim3 grid((unsigned)T, (F / 8 + 255) / 256);
+  swiglu_fwd_kernel<<<grid, 256, 0, stream>>>(gu, h, F);
   return 0;
 }
 int swiglu_bwd(const bf16_t* gu, const bf16_t* dh, bf16_t* dgu, int64_t T, int F, hipStream_t stream) {
   if (F % 8) return -1;
-  if (T * (F / 8) >= (1ll << 31)) return -3;
-  swiglu_bwd_kernel<<<stream_grid(T * (F / 8), 256), 256, 0, stream>>>(gu, dh, dgu, T, F);
+  if (T == 0) return 0;
+  if (T >= (1ll << 31)) return -3;
+  const dim3 grid((unsigned)T, (F / 8 + 255) / 256);
+  swiglu_bwd_kernel<<<grid, 256, 0, stream>>>(gu, dh, dgu, F);
   return 0;
 }
 

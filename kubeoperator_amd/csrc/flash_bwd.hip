@@ -157,9 +157,14 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
 
   // one barrier per stage: it publishes stage qt AND proves every wave is done with stage qt-1, whose slot
   // the DMA of stage qt+1 then refills (prefetch distance: one stage of compute)
+  // the previous stage's dS stores are this wave's 16 youngest vector-memory ops: they may stay in flight
+  // across the barrier (only this stage's DMA, issued before them, must have landed)
+  bool stored = false;
   for (int qt = qt0; qt < nqt; ++qt) {
     const int stage = (qt - qt0) & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (WDS && stored) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stored = false;
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (qt + 1 < nqt) issue(qt + 1, stage ^ 1);
@@ -236,6 +241,7 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
           asm volatile("global_store_short %0, %1, %2" ::"v"(loff), "v"(w), "s"(ra) : "memory");
           asm volatile("global_store_short_d16_hi %0, %1, %2" ::"v"(loff), "v"(w), "s"(rb) : "memory");
         }
+        stored = true;
       }
       // transposed dO / Q reads: rows 16s + 4hh + tq (+8) are tb_lane[(row0>>3)&1] + RB*(row0>>3), column
       // block dt is +512*dt (sub-tiled image, all immediates)

@@ -215,6 +215,87 @@ __global__ void __launch_bounds__(256) col_reduce_kernel(const float* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Row-per-wave forward (H a multiple of 512, up to 4096 = Llama-3-8B): a 64-lane wave owns a whole row, each
+// lane holds NV = H/512 16-byte chunks (chunk c = lane + 64v, so every v is one contiguous 1 KiB wave
+// access), and the row statistics are wave reductions -- no LDS round trip and no __syncthreads per row,
+// and 2*NV loads in flight per lane instead of 2. Four rows per 256-thread block. (The backward keeps the
+// block-per-row form: a row-per-wave backward holds 8*NV fp32 weight-gradient partials per lane on top of
+// the row data and drops to 2 waves per SIMD -- measured slower.)
+// ---------------------------------------------------------------------------------------------------
+template <int NV, bool LN, bool HAS_RES>
+__global__ void __launch_bounds__(256) norm_fwd_wave_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ r,
+                                                            const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
+                                                            bf16_t* __restrict__ y, bf16_t* __restrict__ s_out,
+                                                            float* __restrict__ rstd_out, float* __restrict__ mean_out,
+                                                            int rows, int H, float eps) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const float inv_h = 1.f / (float)H;
+  for (int row = blockIdx.x * 4 + wv; row < rows; row += gridDim.x * 4) {
+    const u32x4* xr = reinterpret_cast<const u32x4*>(x + (size_t)row * H);
+    u32x4 xv[NV], rv[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) xv[v] = xr[lane + 64 * v];
+    if (HAS_RES) {
+      const u32x4* rr = reinterpret_cast<const u32x4*>(r + (size_t)row * H);
+#pragma unroll
+      for (int v = 0; v < NV; ++v) rv[v] = rr[lane + 64 * v];
+    }
+    float f[NV][8];
+    float acc = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      unpack8(xv[v], f[v]);
+      if (HAS_RES) {
+        float g[8];
+        unpack8(rv[v], g);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) f[v][i] += g[i];
+        // the residual stream is carried in bf16: normalise exactly what is stored
+        const u32x4 pk = pack8(f[v]);
+        reinterpret_cast<u32x4*>(s_out + (size_t)row * H)[lane + 64 * v] = pk;
+        unpack8(pk, f[v]);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc += LN ? f[v][i] : f[v][i] * f[v][i];
+    }
+    float mean = 0.f;
+    if (LN) {
+      mean = wave_sum(acc) * inv_h;
+      acc = 0.f;
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float d = f[v][i] - mean;
+          acc += d * d;
+        }
+    }
+    const float rstd = rsqrtf(wave_sum(acc) * inv_h + eps);
+    if (lane == 0) {
+      rstd_out[row] = rstd;
+      if (LN) mean_out[row] = mean;
+    }
+    u32x4* yr = reinterpret_cast<u32x4*>(y + (size_t)row * H);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      float wf[8], bf[8], o[8];
+      unpack8(reinterpret_cast<const u32x4*>(w)[lane + 64 * v], wf);
+      if (LN) unpack8(reinterpret_cast<const u32x4*>(b)[lane + 64 * v], bf);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (f[v][i] - mean) * rstd * wf[i] + (LN ? bf[i] : 0.f);
+      yr[lane + 64 * v] = pack8(o);
+    }
+  }
+}
+
+// row-per-wave path: H = 512 * NV, NV in {1, 2, 4, 8}
+static int wave_nv(int H) {
+  if (H % 512 != 0) return 0;
+  const int nv = H / 512;
+  return (nv == 1 || nv == 2 || nv == 4 || nv == 8) ? nv : 0;
+}
+
 static void pick_geom(int H, int& threads, int& nv) {
   const int C = H / 8;
   threads = C >= 256 ? 256 : ((C + 63) / 64) * 64;
@@ -236,6 +317,25 @@ static void pick_geom(int H, int& threads, int& nv) {
 int norm_fwd(const bf16_t* x, const bf16_t* r, const bf16_t* w, const bf16_t* b, bf16_t* y, bf16_t* s_out, float* rstd,
              float* mean, int rows, int H, float eps, bool layernorm, hipStream_t stream) {
   if (H % 8 != 0 || H > 8192) return -1;
+  if (const int wn = wave_nv(H)) {
+    const int grid = (rows + 3) / 4 < 4096 ? (rows + 3) / 4 : 4096;
+#define NORM_FWD_WAVE(NVv)                                                                                  \
+    if (wn == NVv) {                                                                                        \
+      if (layernorm) {                                                                                      \
+        if (r) norm_fwd_wave_kernel<NVv, true, true><<<grid, 256, 0, stream>>>(x, r, w, b, y, s_out, rstd, mean, rows, H, eps); \
+        else norm_fwd_wave_kernel<NVv, true, false><<<grid, 256, 0, stream>>>(x, r, w, b, y, s_out, rstd, mean, rows, H, eps); \
+      } else {                                                                                              \
+        if (r) norm_fwd_wave_kernel<NVv, false, true><<<grid, 256, 0, stream>>>(x, r, w, b, y, s_out, rstd, mean, rows, H, eps); \
+        else norm_fwd_wave_kernel<NVv, false, false><<<grid, 256, 0, stream>>>(x, r, w, b, y, s_out, rstd, mean, rows, H, eps); \
+      }                                                                                                     \
+      return 0;                                                                                             \
+    }
+    NORM_FWD_WAVE(1)
+    NORM_FWD_WAVE(2)
+    NORM_FWD_WAVE(4)
+    NORM_FWD_WAVE(8)
+#undef NORM_FWD_WAVE
+  }
   int threads, nv;
   pick_geom(H, threads, nv);
   const int grid = rows < 8192 ? rows : 8192;
@@ -247,7 +347,7 @@ int norm_fwd(const bf16_t* x, const bf16_t* r, const bf16_t* w, const bf16_t* b,
 }
 
 #define NORM_BWD_DISPATCH(NVv)                                                                               \
-  if (nv == NVv) {                                                                                           \
+  if (!done && nv == NVv) {                                                                                           \
     if (layernorm) {                                                                                         \
       if (dres) norm_bwd_kernel<NVv, true, true><<<grid, threads, 0, stream>>>(dy, s, w, rstd, mean, dres, dx, part, part + (size_t)grid * H, rows, H); \
       else norm_bwd_kernel<NVv, true, false><<<grid, threads, 0, stream>>>(dy, s, w, rstd, mean, dres, dx, part, part + (size_t)grid * H, rows, H); \
@@ -264,10 +364,10 @@ int norm_bwd(const bf16_t* dy, const bf16_t* s, const bf16_t* w, const float* rs
              const bf16_t* dres, bf16_t* dx, float* part, bf16_t* dw, bf16_t* db, int rows, int H, bool layernorm,
              int accumulate, hipStream_t stream) {
   if (H % 8 != 0 || H > 8192) return -1;
-  int threads, nv;
-  pick_geom(H, threads, nv);
   const int grid = norm_bwd_partial_rows(rows);
   bool done = false;
+  int threads, nv;
+  pick_geom(H, threads, nv);
   NORM_BWD_DISPATCH(1)
   NORM_BWD_DISPATCH(2)
   NORM_BWD_DISPATCH(3)

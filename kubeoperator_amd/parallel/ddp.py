@@ -91,9 +91,15 @@ class DataParallel:
         return self._gather(b, a, e, async_op=True)
 
     def _gather(self, b: Bucket, a: int, e: int, async_op: bool):
-        """In-place all-gather of the bucket's updated pieces (RCCL on GPU; gloo runs the same call on CPU)."""
-        st = self.store
-        return dist.all_gather_into_tensor(st.params[b.start:b.end], st.params[a:e], async_op=async_op)
+        """In-place all-gather of the bucket's updated pieces (RCCL on GPU; gloo runs the same call on CPU).
+
+        Through ``params.data``: the parameters are views of the flat buffer and share ITS autograd version
+        counter, so a collective writing bucket Y through a plain view would bump the version of the bucket-X
+        weights the current forward has already saved for backward (gloo completes CUDA gathers with a
+        ``copy_`` at ``wait()``, i.e. mid-forward when the gate is resolved). The ordering that matters --
+        bucket Y written before any kernel reads it -- is the gate's stream dependency, not autograd's."""
+        pd = self.store.params.data
+        return dist.all_gather_into_tensor(pd[b.start:b.end], pd[a:e], async_op=async_op)
 
     def norm_allreduce(self):
         if self.mode == "zero1" and self.world > 1:

@@ -31,27 +31,29 @@ def init_distributed(device: str = "auto", timeout_s: int = 1800) -> DistInfo:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = (device == "cuda") or (device == "auto" and torch.cuda.is_available())
+    # rehearsal knobs (tests): several ranks on one GPU need gloo (RCCL refuses two ranks on one device)
+    dev_index = int(os.environ.get("KOP_DEVICE_INDEX", local))
     if use_gpu:
-        torch.cuda.set_device(local)
-        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev_index)
+        dev = torch.device("cuda", dev_index)
     else:
         dev = torch.device("cpu")
     backend = "none"
     if world > 1 and not dist.is_initialized():
-        backend = "nccl" if use_gpu else "gloo"
+        backend = os.environ.get("KOP_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         kw = {}
         init = os.environ.get("KOP_DIST_INIT")  # e.g. file:///tmp/x (tests: no TCP port race)
         if init:
             kw["init_method"] = init
-        if use_gpu:
+        if use_gpu and backend == "nccl":
             kw["device_id"] = dev
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
     elif dist.is_initialized():
         backend = dist.get_backend()
-    return DistInfo(rank, local, world, backend, dev)
+    return DistInfo(rank, dev_index if use_gpu else local, world, backend, dev)
 
 
 def barrier(info: DistInfo) -> None:

@@ -69,7 +69,7 @@ def _ddp_worker(rank, world, init, mode, out_q):
     torch.set_num_threads(1)
     from kubeoperator_amd.parallel.dist import init_distributed, shutdown
     info = init_distributed("cpu")
-    tr = Trainer(_tc(micro_batch=2, dp_mode=mode), info)
+    tr = Trainer(_tc(micro_batch=2, dp_mode=mode, lr=1e-1, eps=1.0), info)
     for step in range(3):
         ids, tgt = _batch(tr, seed=step, mb=2 * world)
         tr.train_step([(ids[2 * rank:2 * rank + 2], tgt[2 * rank:2 * rank + 2])])
@@ -92,10 +92,16 @@ def test_data_parallel_gloo_matches_single_process(mode, world, tmp_path):
     for p in procs:
         p.join(120)
         assert p.exitcode == 0
-    single = Trainer(_tc(micro_batch=2 * world), DistInfo())
+    single = Trainer(_tc(micro_batch=2 * world, lr=1e-1, eps=1.0), DistInfo())
+    init = _unpadded(single)
     for step in range(3):
         single.train_step([_batch(single, seed=step, mb=2 * world)])
-    torch.testing.assert_close(got, _unpadded(single), atol=2e-2, rtol=0)
+    want = _unpadded(single)
+    # eps >> |grad| keeps Adam's update ~linear in the gradient (no +-lr sign flips on near-zero gradients),
+    # so the relative error of the whole update is bf16 reduction noise (~1 %) unless an update is lost,
+    # doubled or stale (O(1))
+    rel = ((got - want).norm() / (want - init).norm()).item()
+    assert rel < 0.05, rel
 
 
 def test_checkpoint_resume_is_exact(tmp_path):

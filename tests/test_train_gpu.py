@@ -35,3 +35,4 @@ def test_overlapped_optimizer_matches_serial():
     assert diff <= 4 * noise, (diff, noise)
     if noise == 0:
         assert torch.equal(l_ser, l_ovl) and torch.equal(ser.store.params, ovl.store.params)
+

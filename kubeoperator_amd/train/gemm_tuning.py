@@ -25,7 +25,7 @@ def setup(mode: str = "use", path: str | None = None, rank: int = 0) -> str:
     if mode == "off" or not torch.cuda.is_available():
         return "off"
     tun = torch.cuda.tunable
-    path = path or results_path()
+    path = path or os.environ.get("KOP_GEMM_RESULTS") or results_path()
     if mode == "use" and not os.path.exists(path):
         return "off (no tuned results)"
     tun.enable(True)

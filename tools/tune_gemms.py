@@ -42,6 +42,8 @@ def main():
     tun.tuning_enable(False)
     tun.record_untuned_enable(True)
     tun.set_filename(out, insert_device_ordinal=False)
+    if os.path.exists(out):
+        tun.read_file(out)  # keep the committed winners: only shapes without one are recorded and tuned
 
     info = init_distributed("auto")
     tr = Trainer(TrainConfig(model=a.model, micro_batch=a.mbs, seq_len=a.seq, warmup_steps=10, total_steps=100), info)

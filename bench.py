@@ -5,9 +5,11 @@ one rank per GPU over RCCL. W untimed warmup steps, then EXACTLY K timed optimiz
 barrier + device synchronize on both sides; the MAX step time over ranks is used; rank 0 prints one JSON
 line. ``value`` is the whole-job throughput (sum over ranks = N x per-rank tokens / max time).
 
-Every timed step is a complete training step: forward through all 32 layers, cross-entropy over the full
-128,256 vocabulary, backward, bucketed RCCL gradient collectives (N > 1), gradient clipping and the fused
-AdamW update of all 8.03 B parameters. Weights are random-init, tokens synthetic (no network / datasets).
+Every timed step is a complete training step: ``--accum`` micro-batches of forward through all 32 layers,
+cross-entropy over the full 128,256 vocabulary and backward (gradients accumulated in the flat bf16 buffer),
+bucketed RCCL gradient collectives overlapped with the last backward (N > 1; ZeRO-1 by default), gradient
+clipping and the fused AdamW update of all 8.03 B parameters. Weights are random-init, tokens synthetic (no
+network / datasets).
 """
 from __future__ import annotations
 
@@ -30,7 +32,10 @@ def main() -> int:
     ap.add_argument("--model", default="llama3_8b")
     ap.add_argument("--seq", type=int, default=8192)
     ap.add_argument("--mbs", type=int, default=1, help="micro-batch (sequences) per rank")
-    ap.add_argument("--accum", type=int, default=1, help="gradient-accumulation micro-batches per step")
+    ap.add_argument("--accum", type=int, default=4,
+                    help="gradient-accumulation micro-batches per optimizer step (default 4: 32k tokens per GPU per "
+                         "step, 256k at 8 GPUs -- still far below the ~4M-token global batches Llama-3 pretraining "
+                         "uses; one step per 8k-token micro-batch would be dominated by the 28 B/param update)")
     ap.add_argument("--dp", default="auto", choices=["auto", "allreduce", "zero1"],
                     help="auto: ZeRO-1 when WORLD_SIZE > 1 (reduce-scatter + sharded AdamW + all-gather: the same "
                          "bytes on xGMI as an all-reduce, 1/N of the optimizer's HBM traffic), else plain")

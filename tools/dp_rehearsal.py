@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def global_batch(vocab, world, step, mbs, seq):
-    g = torch.Generator().manual_seed(100 + step)
+    g = torch.Generator().manual_seed(100 + step)  # step = optimizer step * accum + micro-batch
     ids = torch.randint(0, vocab, (mbs * world, seq + 1), generator=g)
     return ids[:, :-1].contiguous(), ids[:, 1:].contiguous()
 
@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--seq", type=int, default=256)
     ap.add_argument("--mbs", type=int, default=2)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--accum", type=int, default=1, help="gradient-accumulation micro-batches per step")
     ap.add_argument("--bucket-mb", type=int, default=1)
     ap.add_argument("--lr", type=float, default=1e-1, help="large, so a missing or double update is visible")
     ap.add_argument("--eps", type=float, default=1.0,
@@ -49,12 +50,12 @@ def main():
     world, rank = info.world, info.rank
     kw = dict(model=a.model, seq_len=a.seq, warmup_steps=1, total_steps=10, bucket_mb=a.bucket_mb,
               overlap_optimizer=True, lr=a.lr, eps=a.eps)
-    tr = Trainer(TrainConfig(micro_batch=a.mbs, dp_mode=a.mode, **kw), info)
+    tr = Trainer(TrainConfig(micro_batch=a.mbs, grad_accum=a.accum, dp_mode=a.mode, **kw), info)
     init = flat(tr)
+    sl = slice(a.mbs * rank, a.mbs * (rank + 1))
     for step in range(a.steps):
-        ids, tgt = global_batch(tr.cfg.vocab_size, world, step, a.mbs, a.seq)
-        sl = slice(a.mbs * rank, a.mbs * (rank + 1))
-        tr.train_step([(ids[sl].to(info.device), tgt[sl].to(info.device))])
+        mb = [global_batch(tr.cfg.vocab_size, world, step * a.accum + i, a.mbs, a.seq) for i in range(a.accum)]
+        tr.train_step([(ids[sl].to(info.device), tgt[sl].to(info.device)) for ids, tgt in mb])
     tr.store.await_all()
     if info.device.type == "cuda":
         torch.cuda.synchronize()
@@ -62,10 +63,10 @@ def main():
     shutdown(info)
     if rank != 0:
         return 0
-    one = Trainer(TrainConfig(micro_batch=a.mbs * world, **kw), DistInfo(0, 0, 1, "none", info.device))
+    one = Trainer(TrainConfig(micro_batch=a.mbs * world, grad_accum=a.accum, **kw), DistInfo(0, 0, 1, "none", info.device))
     for step in range(a.steps):
-        ids, tgt = global_batch(one.cfg.vocab_size, world, step, a.mbs, a.seq)
-        one.train_step([(ids.to(info.device), tgt.to(info.device))])
+        mb = [global_batch(one.cfg.vocab_size, world, step * a.accum + i, a.mbs, a.seq) for i in range(a.accum)]
+        one.train_step([(ids.to(info.device), tgt.to(info.device)) for ids, tgt in mb])
     one.store.await_all()
     want = flat(one)
     # relative error of the whole update: a lost, doubled or stale bucket update makes it O(1); bf16
@@ -73,7 +74,7 @@ def main():
     upd = (want - init).norm().item()
     rel = (got - want).norm().item() / max(upd, 1e-30)
     ok = rel < 0.05
-    print(json.dumps({"rehearsal": f"dp{world}-{a.mode}", "model": a.model, "rel_update_error": rel,
+    print(json.dumps({"rehearsal": f"dp{world}-{a.mode}", "accum": a.accum, "model": a.model, "rel_update_error": rel,
                       "update_norm": upd, "max_abs_param_diff": (got - want).abs().max().item(), "ok": ok,
                       "buckets": len(tr.store.buckets), "optimizer_overlap": tr.opt.overlap}), flush=True)
     return 0 if ok else 1

@@ -5,12 +5,12 @@ set -o pipefail
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 port=29560
-for cfg in "2 zero1" "2 allreduce" "4 zero1" "4 allreduce"; do
+for cfg in "2 zero1 1" "2 allreduce 1" "4 zero1 1" "4 allreduce 1" "2 zero1 2" "4 zero1 4"; do
   set -- $cfg
   port=$((port + 1))
   timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node $1 --master-addr 127.0.0.1 \
-    --master-port $port tools/dp_rehearsal.py --mode $2 > gpurun_out/dp_$1_$2.log 2>&1
-  rc=$?; echo "dp$1 $2 rc=$rc $(grep rehearsal gpurun_out/dp_$1_$2.log)"; [ $rc -eq 0 ] || exit $rc
+    --master-port $port tools/dp_rehearsal.py --mode $2 --accum $3 > gpurun_out/dp_$1_$2_a$3.log 2>&1
+  rc=$?; echo "dp$1 $2 accum$3 rc=$rc $(grep rehearsal gpurun_out/dp_$1_$2_a$3.log)"; [ $rc -eq 0 ] || exit $rc
 done
 # Llama-3 1B proxy (vocab 128256, hidden 2048) with the production 512 MiB buckets
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
@@ -20,4 +20,9 @@ rc=$?; echo "dp2 zero1 1b rc=$rc $(grep rehearsal gpurun_out/dp_2_zero1_1b.log)"
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
   --master-port 29591 tools/dp_rehearsal.py --mode allreduce --model llama3_1b_proxy --seq 2048 --mbs 1 --bucket-mb 512 \
   > gpurun_out/dp_2_allreduce_1b.log 2>&1
-rc=$?; echo "dp2 allreduce 1b rc=$rc $(grep rehearsal gpurun_out/dp_2_allreduce_1b.log)"; exit $rc
+rc=$?; echo "dp2 allreduce 1b rc=$rc $(grep rehearsal gpurun_out/dp_2_allreduce_1b.log)"; [ $rc -eq 0 ] || exit $rc
+# bench.py itself, launched exactly as the driver launches it, 2 ranks sharing the card (throughput meaningless)
+KOP_DIST_BACKEND=gloo KOP_DEVICE_INDEX=0 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+  --master-addr 127.0.0.1 --master-port 29592 bench.py --gpus 2 --steps 2 --warmup 1 --model llama3_1b_proxy --seq 2048 \
+  > gpurun_out/dp_bench_2.log 2>&1
+rc=$?; echo "bench dp2 rc=$rc $(grep metric gpurun_out/dp_bench_2.log | cut -c1-200)"; exit $rc

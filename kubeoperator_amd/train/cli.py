@@ -1,7 +1,7 @@
 """Training entry point of the bundled chart: ``torchrun --nproc-per-node=8 -m kubeoperator_amd.train.cli``.
 
 Logs one JSON line per ``--log-every`` steps on rank 0 (step, loss, grad norm, lr, step time, tokens/s,
-TFLOP/s per GPU); checkpoints every ``--ckpt-every`` steps and resumes from the newest complete
+TFLOP/s per GPU), optionally also as Prometheus gauges on ``--metrics-port`` (``train.metrics``); checkpoints every ``--ckpt-every`` steps and resumes from the newest complete
 checkpoint with ``--resume`` (elastic restarts via ``torchrun --max-restarts`` then continue where the
 failed attempt left off).
 """
@@ -22,7 +22,8 @@ def main(argv=None) -> int:
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5, help="LR warmup steps")
     ap.add_argument("--lr", type=float, default=3e-4)
-    ap.add_argument("--dp", default="allreduce", choices=["allreduce", "zero1"])
+    ap.add_argument("--dp", default="auto", choices=["auto", "allreduce", "zero1"],
+                    help="auto: ZeRO-1 when WORLD_SIZE > 1")
     ap.add_argument("--bucket-mb", type=int, default=512)
     ap.add_argument("--data", default="synthetic", help="'synthetic' or a flat uint16 token file")
     ap.add_argument("--ckpt-dir", default="")
@@ -32,6 +33,7 @@ def main(argv=None) -> int:
     ap.add_argument("--device", default="auto")
     ap.add_argument("--gemm-tuning", default="use", choices=["off", "use", "tune"])
     ap.add_argument("--overlap-opt", type=int, default=1, choices=[0, 1])
+    ap.add_argument("--metrics-port", type=int, default=0, help="rank 0 serves Prometheus metrics here (0: off)")
     a = ap.parse_args(argv)
 
     import torch
@@ -42,6 +44,8 @@ def main(argv=None) -> int:
     from .trainer import TrainConfig, Trainer, lr_at
 
     info = init_distributed(a.device)
+    if a.dp == "auto":
+        a.dp = "zero1" if info.world > 1 else "allreduce"
     from . import gemm_tuning
 
     gemm_tuning.setup(a.gemm_tuning, rank=info.rank)
@@ -59,6 +63,12 @@ def main(argv=None) -> int:
                                 start_batch=tr.step * a.accum)
     cuda = info.device.type == "cuda"
     flops_tok = tr.cfg.flops_per_token(a.seq)
+    metrics = None
+    if a.metrics_port and info.is_main:
+        from .metrics import TrainMetrics
+
+        metrics = TrainMetrics(a.metrics_port, {"model": a.model, "world": str(info.world), "dp": a.dp})
+    comm_seen = 0
     while tr.step < a.steps:
         t0 = time.perf_counter()
         loss = tr.train_step(data.batches(a.accum))
@@ -68,12 +78,20 @@ def main(argv=None) -> int:
             dt = all_reduce_max(time.perf_counter() - t0, info)
             toks = info.world * tr.tokens_per_step / dt
             if info.is_main:
-                print(json.dumps({"step": tr.step, "loss": round(float(loss), 4),
-                                  "grad_norm": round(float(tr.opt.last_grad_norm), 4),
-                                  "lr": lr_at(tr.step - 1, tc), "step_s": round(dt, 4), "tokens_per_s": round(toks, 1),
-                                  "tflops_per_gpu": round(flops_tok * toks / info.world / 1e12, 1)}), flush=True)
+                rec = {"step": tr.step, "loss": round(float(loss), 4),
+                       "grad_norm": round(float(tr.opt.last_grad_norm), 4),
+                       "lr": lr_at(tr.step - 1, tc), "step_s": round(dt, 4), "tokens_per_s": round(toks, 1),
+                       "tflops_per_gpu": round(flops_tok * toks / info.world / 1e12, 1)}
+                print(json.dumps(rec), flush=True)
+                if metrics is not None:
+                    metrics.observe(step=rec["step"], loss=rec["loss"], grad_norm=rec["grad_norm"], lr=rec["lr"],
+                                    step_s=dt, tokens_per_s=toks, tflops=rec["tflops_per_gpu"],
+                                    comm_bytes_delta=tr.dp.comm_bytes - comm_seen)
+                    comm_seen = tr.dp.comm_bytes
         if a.ckpt_dir and a.ckpt_every and tr.step % a.ckpt_every == 0:
             checkpoint.save(tr, a.ckpt_dir, info)
+    if metrics is not None:
+        metrics.close()
     shutdown(info)
     return 0
 

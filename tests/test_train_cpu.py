@@ -145,3 +145,35 @@ def test_native_prefetcher_matches_python_path(tmp_path):
     # resume: a fresh loader started at batch 20 continues the same stream
     res = TokenFileDataset(path, 3, 128, "cpu", seed=7, rank=1, start_batch=20)
     assert torch.equal(res.next()[0], py.next()[0])
+
+
+def test_train_metrics_endpoint():
+    import socket
+    import urllib.request
+
+    from kubeoperator_amd.train.metrics import TrainMetrics
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    m = TrainMetrics(port, {"model": "tiny_llama", "world": "1", "dp": "allreduce"})
+    try:
+        m.observe(step=3, loss=2.5, grad_norm=0.75, lr=1e-4, step_s=0.5, tokens_per_s=1234.0, tflops=1.5,
+                  comm_bytes_delta=4096)
+        body = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=10).read().decode()
+    finally:
+        m.close()
+    assert 'kop_train_tokens_per_second{dp="allreduce",model="tiny_llama",world="1"} 1234.0' in body
+    assert "kop_train_step_seconds" in body and "kop_train_collective_bytes_total" in body
+
+
+def test_train_cli_runs_and_logs(capsys):
+    import json
+
+    from kubeoperator_amd.train import cli
+
+    assert cli.main(["--model", "tiny_llama", "--seq", "64", "--steps", "2", "--accum", "2", "--device", "cpu",
+                     "--gemm-tuning", "off"]) == 0
+    recs = [json.loads(ln) for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")]
+    assert [r["step"] for r in recs] == [1, 2] and all(r["tokens_per_s"] > 0 for r in recs)

@@ -422,15 +422,22 @@ __global__ void __launch_bounds__(512, 1) fa_fwd8_kernel(const bf16_t* __restric
   const float lt = l + __shfl_xor(l, 32, 64);
   const float inv = 1.f / lt;
   if (hh == 0) lse[((int64_t)(b * Hq + hq)) * S + q0w + r] = (m + __log2f(lt)) * 0.69314718056f;
-  bf16_t* op = o + (int64_t)(b * S + q0w + r) * os + hq * D;
+  // widened store tail (guide T21): lane r holds columns 8g..8g+3 of row r, lane r+32 columns 8g+4..8g+7; one
+  // v_permlane32_swap per dword of a (g, g+1) pair leaves lane r with columns 16p..16p+7 and lane r+32 with
+  // 16p+8..16p+15, so each lane writes 16 B per pair: 8 dwordx4 stores instead of 16 dwordx2
+  bf16_t* op = o + (int64_t)(b * S + q0w + r) * os + hq * D + 8 * hh;
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) {
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      u32x2 w;
-      w[0] = pack2(oacc[dt][4 * g4] * inv, oacc[dt][4 * g4 + 1] * inv);
-      w[1] = pack2(oacc[dt][4 * g4 + 2] * inv, oacc[dt][4 * g4 + 3] * inv);
-      *reinterpret_cast<u32x2*>(op + dt * 32 + 8 * g4 + 4 * hh) = w;
+    for (int pr = 0; pr < 2; ++pr) {
+      const int g0 = 2 * pr, g1 = 2 * pr + 1;
+      const uint32_t a0 = pack2(oacc[dt][4 * g0] * inv, oacc[dt][4 * g0 + 1] * inv);
+      const uint32_t a1 = pack2(oacc[dt][4 * g0 + 2] * inv, oacc[dt][4 * g0 + 3] * inv);
+      const uint32_t b0 = pack2(oacc[dt][4 * g1] * inv, oacc[dt][4 * g1 + 1] * inv);
+      const uint32_t b1 = pack2(oacc[dt][4 * g1 + 2] * inv, oacc[dt][4 * g1 + 3] * inv);
+      const auto s0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+      const auto s1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+      *reinterpret_cast<u32x4*>(op + dt * 32 + 16 * pr) = u32x4{s0[0], s1[0], s0[1], s1[1]};
     }
   }
 }

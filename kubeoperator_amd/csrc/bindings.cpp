@@ -80,7 +80,7 @@ Tensor norm_bwd(const Tensor& dy, const Tensor& s, const Tensor& w, const Tensor
   const int H = (int)s.size(-1);
   const int rows = (int)(s.numel() / H);
   auto dx = at::empty_like(s);
-  const int parts = kop::norm_bwd_partial_rows(rows);
+  const int parts = kop::norm_bwd_partial_rows(rows, H);
   auto part = at::empty({(layernorm ? 2 : 1) * (int64_t)parts * H}, s.options().dtype(at::kFloat));
   rc(kop::norm_bwd(bp(dy), bp(s), bp(w), rstd.data_ptr<float>(),
                    mean.has_value() && mean->defined() ? mean->data_ptr<float>() : nullptr, cbp(dres), bp(dx),

@@ -12,7 +12,7 @@ typedef uint16_t bf16_t;
 // norms.hip
 int norm_fwd(const bf16_t* x, const bf16_t* r, const bf16_t* w, const bf16_t* b, bf16_t* y, bf16_t* s_out, float* rstd,
              float* mean, int rows, int H, float eps, bool layernorm, hipStream_t stream);
-int norm_bwd_partial_rows(int rows);
+int norm_bwd_partial_rows(int rows, int H);
 int norm_bwd(const bf16_t* dy, const bf16_t* s, const bf16_t* w, const float* rstd, const float* mean,
              const bf16_t* dres, bf16_t* dx, float* part, bf16_t* dw, bf16_t* db, int rows, int H, bool layernorm,
              int accumulate, hipStream_t stream);

@@ -358,13 +358,18 @@ int norm_fwd(const bf16_t* x, const bf16_t* r, const bf16_t* w, const bf16_t* b,
     done = true;                                                                                             \
   }
 
-int norm_bwd_partial_rows(int rows) { return rows < 512 ? rows : 512; }
+// Blocks of the backward = fp32 weight-gradient partial rows. Narrow rows (GPT-2's 768) need more blocks to
+// keep enough rows in flight: 512 blocks x 2 waves was latency-bound at ~1.5 TB/s.
+int norm_bwd_partial_rows(int rows, int H) {
+  const int cap = H <= 1024 ? 2048 : 512;
+  return rows < cap ? rows : cap;
+}
 
 int norm_bwd(const bf16_t* dy, const bf16_t* s, const bf16_t* w, const float* rstd, const float* mean,
              const bf16_t* dres, bf16_t* dx, float* part, bf16_t* dw, bf16_t* db, int rows, int H, bool layernorm,
              int accumulate, hipStream_t stream) {
   if (H % 8 != 0 || H > 8192) return -1;
-  const int grid = norm_bwd_partial_rows(rows);
+  const int grid = norm_bwd_partial_rows(rows, H);
   bool done = false;
   int threads, nv;
   pick_geom(H, threads, nv);

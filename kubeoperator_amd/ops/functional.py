@@ -59,10 +59,14 @@ def _mm_into(a, b, out, accumulate):
 
 
 # weight gradients dW = dY^T X through the forward ("TN") GEMM layout: hipBLASLt runs the strided "NT"
-# form at ~1.15 PF/s and the K-contiguous form at ~1.55 PF/s on MI355X; two HIP transposes at HBM speed
-# cost far less than the difference (tools/bench_gemm_layouts.py, csrc/transpose.hip).
-_DW_LAYOUT = os.environ.get("KOP_DW_LAYOUT", "tn")
+# form at ~1.15 PF/s and the K-contiguous form at ~1.55 PF/s on MI355X at Llama-3-8B widths; two HIP
+# transposes at HBM speed cost far less than the difference there (tools/bench_gemm_layouts.py,
+# csrc/transpose.hip). At GPT-2-small widths (768-3072) the GEMMs are short and the transposes are not
+# repaid: the step is 4.6 % faster without them (profiles/r1_experiments.md). "auto" picks per GEMM by
+# the narrower of its two output dimensions.
+_DW_LAYOUT = os.environ.get("KOP_DW_LAYOUT", "auto")
 _DW_TN_MIN_ROWS = 1024
+_DW_TN_MIN_WIDTH = 2048
 
 
 def _rows_ok(t: torch.Tensor) -> bool:
@@ -79,8 +83,9 @@ def transpose(x: torch.Tensor) -> torch.Tensor:
 
 def _dw_into(dy2, x2, out, accumulate):
     """out (+)= dy2^T @ x2, the reduction running over the token rows."""
-    if (_DW_LAYOUT == "tn" and dy2.shape[0] >= _DW_TN_MIN_ROWS and dy2.shape[0] % 8 == 0 and _rows_ok(dy2)
-            and _rows_ok(x2)):
+    wide = min(dy2.shape[1], x2.shape[1]) >= _DW_TN_MIN_WIDTH
+    if ((_DW_LAYOUT == "tn" or (_DW_LAYOUT == "auto" and wide)) and dy2.shape[0] >= _DW_TN_MIN_ROWS
+            and dy2.shape[0] % 8 == 0 and _rows_ok(dy2) and _rows_ok(x2)):
         _mm_into(transpose(dy2), transpose(x2).t(), out, accumulate)
     else:
         _mm_into(dy2.t(), x2, out, accumulate)

@@ -270,19 +270,21 @@ def test_transpose_exact(R, C):
     assert torch.equal(y, x.t())
 
 
-def test_weight_grad_tn_layout_matches_nt():
+@pytest.mark.parametrize("layout", ["tn", "nt", "auto"])
+def test_weight_grad_tn_layout_matches_nt(layout, monkeypatch):
     import kubeoperator_amd.ops.functional as kf
 
+    monkeypatch.setattr(kf, "_DW_LAYOUT", layout)
     torch.manual_seed(11)
-    T, N, K = 2048, 768, 512
-    x = torch.randn(T, K, device=DEV).to(torch.bfloat16)
-    dy = torch.randn(T, N, device=DEV).to(torch.bfloat16)
-    out = torch.empty(N, K, device=DEV, dtype=torch.bfloat16)
-    kf._dw_into(dy, x, out, False)
-    ref = dy.float().t() @ x.float()
-    assert rel_err(out, ref) < 1e-2
-    kf._dw_into(dy, x, out, True)
-    assert rel_err(out, 2 * ref) < 1e-2
+    for T, N, K in ((2048, 768, 512), (2048, 2048, 4096)):
+        x = torch.randn(T, K, device=DEV).to(torch.bfloat16)
+        dy = torch.randn(T, N, device=DEV).to(torch.bfloat16)
+        out = torch.empty(N, K, device=DEV, dtype=torch.bfloat16)
+        kf._dw_into(dy, x, out, False)
+        ref = dy.float().t() @ x.float()
+        assert rel_err(out, ref) < 1e-2
+        kf._dw_into(dy, x, out, True)
+        assert rel_err(out, 2 * ref) < 1e-2
 
 
 @pytest.mark.parametrize("variant", [10, 9, 8])

@@ -64,7 +64,8 @@ def main() -> int:
               file=sys.stderr)
     tc = TrainConfig(model=args.model, micro_batch=args.mbs, seq_len=args.seq, grad_accum=args.accum,
                      dp_mode=args.dp, bucket_mb=args.bucket_mb, warmup_steps=10, total_steps=1000,
-                     overlap_optimizer=bool(args.overlap_opt))
+                     overlap_optimizer=bool(args.overlap_opt),
+                     transposed_weights=os.environ.get("KOP_TRANSPOSED_W", "1") != "0")
     trainer = Trainer(tc, info)
     data = SyntheticTokens(trainer.cfg.vocab_size, args.mbs, args.seq, info.device, seed=tc.seed, rank=info.rank)
     cuda = info.device.type == "cuda"

@@ -81,6 +81,20 @@ def transpose(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
+def transpose_into(x: torch.Tensor, out: torch.Tensor) -> None:
+    """out[c, r] = x[r, c] (bf16, HIP kernel on GPU)."""
+    if x.is_cuda:
+        _lib().transpose_(x, out)
+    else:
+        out.copy_(x.t())
+
+
+def _dx(dy2, w):
+    """dX = dY . W through the transposed copy when the flat store keeps one (K-contiguous GEMM layout)."""
+    wt = getattr(w, "wt", None)
+    return torch.mm(dy2, wt.t()) if wt is not None else torch.mm(dy2, w)
+
+
 def _dw_into(dy2, x2, out, accumulate):
     """out (+)= dy2^T @ x2, the reduction running over the token rows."""
     wide = min(dy2.shape[1], x2.shape[1]) >= _DW_TN_MIN_WIDTH
@@ -110,7 +124,7 @@ class _Linear(Function):
     def backward(ctx, dy):
         x2, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, w.shape[0])
-        dx = torch.mm(dy2, w).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
+        dx = _dx(dy2, w).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
         dw = _sink(w, lambda out, acc: _dw_into(dy2, x2, out, acc)) if ctx.needs_input_grad[1] else None
         db = None
         if ctx.has_b and ctx.needs_input_grad[2]:
@@ -375,7 +389,7 @@ class _LMHeadCE(Function):
         g = g.to(torch.float32)
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = (torch.mm(dlogits, w) * g).view(ctx.in_shape)
+            dx = (_dx(dlogits, w) * g).view(ctx.in_shape)
         dw = None
         if ctx.needs_input_grad[1]:
             xg = x2 * g

@@ -132,11 +132,18 @@ class FusedAdamW:
             with torch.cuda.stream(self._stream):
                 for k in self._launch_order():
                     launch(k)
+                    b = self.segments[k].bucket
                     gate = self.on_segment(self.segments[k]) if self.on_segment is not None else None
+                    if self.store.has_transposed:
+                        # the transposed copies follow the bucket's final values (after the ZeRO-1 gather)
+                        if gate is not None:
+                            gate.wait()  # optimizer stream waits for the collective
+                        self.store.refresh_transposed(b)
+                        gate = None
                     if gate is None:
                         gate = torch.cuda.Event()
                         gate.record(self._stream)
-                    self.store.set_gate(self.segments[k].bucket, gate)
+                    self.store.set_gate(b, gate)
         else:
             t = self.step_count
             bc1 = 1 - self.b1 ** t

@@ -36,6 +36,7 @@ class TrainConfig:
     dp_mode: str = "allreduce"  # allreduce | zero1
     bucket_mb: int = 512
     overlap_optimizer: bool = True  # AdamW on its own stream, gated per bucket into the next forward
+    transposed_weights: bool = True  # keep W^T copies of wide weights for the dX GEMMs (GPU only)
     seed: int = 1234
     model_overrides: dict = field(default_factory=dict)
 
@@ -66,6 +67,9 @@ class Trainer:
         self.store.init_weights(seed=tc.seed)
         self.dp = DataParallel(self.store, info, tc.dp_mode)
         self.dp.broadcast_params()
+        if tc.transposed_weights and dev.type == "cuda":
+            self.store.enable_transposed()
+            self.store.refresh_transposed()
         self.opt = FusedAdamW(self.dp.optimizer_segments(), lr=tc.lr, betas=tc.betas, eps=tc.eps,
                               weight_decay=tc.weight_decay, max_grad_norm=tc.grad_clip,
                               grad_scale=self.dp.grad_scale / tc.grad_accum, norm_allreduce=self.dp.norm_allreduce(),
@@ -92,6 +96,8 @@ class Trainer:
         self.dp.finish_grads()
         self.opt.step(lr_at(self.step, self.tc))
         self.dp.after_step()
+        if self.store.has_transposed and not self.opt.overlap:
+            self.store.refresh_transposed()
         self.step += 1
         return torch.stack(losses).mean()
 
@@ -108,4 +114,5 @@ class Trainer:
         self.store.await_all()
         self.store.params.copy_(sd["params"])
         self.opt.load_state_dict(sd["optimizer"])
+        self.store.refresh_transposed()
         self.step = int(sd["step"])

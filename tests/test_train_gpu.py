@@ -36,3 +36,35 @@ def test_overlapped_optimizer_matches_serial():
     if noise == 0:
         assert torch.equal(l_ser, l_ovl) and torch.equal(ser.store.params, ovl.store.params)
 
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_transposed_weight_copies_match(overlap):
+    """dX through the refreshed W^T copies (forced on for the tiny model's 256-wide weights) must train like
+    dX through W: same losses up to GEMM summation order, and every copy equal to its weight's transpose."""
+    from kubeoperator_amd.parallel.dist import DistInfo
+    from kubeoperator_amd.train import SyntheticTokens, TrainConfig, Trainer
+
+    def run(transposed):
+        info = DistInfo(0, 0, 1, "none", torch.device("cuda", 0))
+        tc = TrainConfig(model="tiny_llama", micro_batch=2, seq_len=256, warmup_steps=1, total_steps=10,
+                         bucket_mb=1, overlap_optimizer=overlap, transposed_weights=False)
+        tr = Trainer(tc, info)
+        if transposed:
+            assert tr.store.enable_transposed(min_width=64) > 0
+            tr.store.refresh_transposed()
+        data = SyntheticTokens(tr.cfg.vocab_size, 2, 256, info.device, seed=5)
+        losses = torch.stack([tr.train_step(data.batches(2)) for _ in range(4)]).float().cpu()
+        tr.store.await_all()
+        torch.cuda.synchronize()
+        return tr, losses
+
+    ref, l_ref = run(False)
+    tt, l_t = run(True)
+    torch.testing.assert_close(l_t, l_ref, atol=2e-2, rtol=0)
+    for name, p in tt.store.named_params():
+        wt = getattr(p, "wt", None)
+        if wt is not None:
+            assert torch.equal(wt, p.detach().t()), name
+    rel = ((tt.store.params.float() - ref.store.params.float()).norm() / ref.store.params.float().norm()).item()
+    assert rel < 1e-2, rel

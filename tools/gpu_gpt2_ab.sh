@@ -1,4 +1,7 @@
+#!/bin/bash
 set -o pipefail
+# GPT-2-small: norm numerics, then the bench with the weight-gradient layout forced to TN (transposes) / NT,
+# alternating, in one box session.
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "norm" > gpurun_out/g2_tests.log 2>&1; echo "norm tests rc=$?"; tail -1 gpurun_out/g2_tests.log

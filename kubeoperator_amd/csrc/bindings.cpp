@@ -90,6 +90,18 @@ Tensor norm_bwd(const Tensor& dy, const Tensor& s, const Tensor& w, const Tensor
   return dx;
 }
 
+void bias_grad_(const Tensor& dy, const Tensor& db, bool accumulate) {
+  check_bf16(dy, "dy");
+  check_bf16(db, "db");
+  TORCH_CHECK(dy.dim() == 2 && dy.is_contiguous() && db.is_contiguous() && db.numel() == dy.size(1),
+              "bias_grad: dy must be a contiguous [rows, H] matrix and db a contiguous [H] vector");
+  check_aligned(dy, "dy");
+  const int rows = (int)dy.size(0), H = (int)dy.size(1);
+  auto part = at::empty({(int64_t)kop::bias_grad_parts(rows, H) * H}, dy.options().dtype(at::kFloat));
+  rc(kop::bias_grad(bp(dy), rows, H, part.data_ptr<float>(), bp(db), accumulate ? 1 : 0, cur_stream()),
+     "bias_grad (H must be a multiple of 8)");
+}
+
 // ------------------------------------------------------------------ elementwise
 void rope_(const Tensor& x, const Tensor& cos_t, const Tensor& sin_t, const c10::optional<Tensor>& pos, int64_t S,
            int64_t nheads, int64_t D, bool inverse) {
@@ -258,6 +270,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("ARCH") = "gfx950";
   m.def("norm_fwd", &norm_fwd);
   m.def("norm_bwd", &norm_bwd);
+  m.def("bias_grad_", &bias_grad_);
   m.def("rope_", &rope_);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);

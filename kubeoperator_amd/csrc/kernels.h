@@ -16,6 +16,8 @@ int norm_bwd_partial_rows(int rows, int H);
 int norm_bwd(const bf16_t* dy, const bf16_t* s, const bf16_t* w, const float* rstd, const float* mean,
              const bf16_t* dres, bf16_t* dx, float* part, bf16_t* dw, bf16_t* db, int rows, int H, bool layernorm,
              int accumulate, hipStream_t stream);
+int bias_grad_parts(int rows, int H);
+int bias_grad(const bf16_t* dy, int rows, int H, float* part, bf16_t* db, int accumulate, hipStream_t stream);
 
 // elementwise.hip
 int rope_inplace(bf16_t* x, const float* cos_t, const float* sin_t, const int* pos, int64_t T, int S, int nheads,

@@ -395,4 +395,72 @@ int norm_bwd(const bf16_t* dy, const bf16_t* s, const bf16_t* w, const float* rs
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Bias gradient of a linear layer, db[c] (+)= sum_r dy[r, c] (GPT-2's biased projections): stage 1 sums a
+// chunk of rows per block into fp32 partials (64 lanes x 16-byte column vectors, 4 row lanes, 4 rows in
+// flight per lane), stage 2 is the norm backward's column reduce. Replaces a generic fp32 reduction + cast.
+// ---------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) bias_partial_kernel(const bf16_t* __restrict__ dy, int rows, int H,
+                                                           int rows_per_part, float* __restrict__ part) {
+  const int H8 = H >> 3;
+  const int c8 = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * rows_per_part;
+  const int r1 = min(rows, r0 + rows_per_part);
+  __shared__ float red[3][64 * 8];
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c8 < H8) {
+    const u32x4* p = reinterpret_cast<const u32x4*>(dy) + c8;
+    int r = r0 + rl;
+    for (; r + 12 < r1; r += 16) {
+      u32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = p[(size_t)(r + 4 * u) * H8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float f[8];
+        unpack8(v[u], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += f[j];
+      }
+    }
+    for (; r < r1; r += 4) {
+      float f[8];
+      unpack8(p[(size_t)r * H8], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += f[j];
+    }
+  }
+  const int lane = threadIdx.x & 63;
+  if (rl > 0) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[rl - 1][j * 64 + lane] = acc[j];
+  }
+  __syncthreads();
+  if (rl == 0 && c8 < H8) {
+    float* o = part + (size_t)blockIdx.y * H + (size_t)c8 * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = acc[j] + red[0][j * 64 + lane] + red[1][j * 64 + lane] + red[2][j * 64 + lane];
+  }
+}
+
+int bias_grad_parts(int rows, int H) {
+  const int gx = (H / 8 + 63) / 64;
+  int p = (2048 + gx - 1) / gx;
+  const int max_p = (rows + 63) / 64;
+  if (p > max_p) p = max_p;
+  if (p < 1) p = 1;
+  const int per = (rows + p - 1) / p;
+  return (rows + per - 1) / per;
+}
+
+int bias_grad(const bf16_t* dy, int rows, int H, float* part, bf16_t* db, int accumulate, hipStream_t stream) {
+  if (H % 8 != 0 || rows <= 0) return -1;
+  const int parts = bias_grad_parts(rows, H);
+  const int per = (rows + parts - 1) / parts;
+  bias_partial_kernel<<<dim3((H / 8 + 63) / 64, parts), 256, 0, stream>>>(dy, rows, H, per, part);
+  col_reduce_kernel<<<(H + 63) / 64, 1024, 0, stream>>>(part, parts, H, db, accumulate);
+  return 0;
+}
+
 }  // namespace kop

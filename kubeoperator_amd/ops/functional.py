@@ -105,6 +105,22 @@ def _dw_into(dy2, x2, out, accumulate):
         _mm_into(dy2.t(), x2, out, accumulate)
 
 
+_BIAS_HIP = os.environ.get("KOP_BIAS_GRAD", "hip") == "hip"
+
+
+def _bias_grad_into(dy2, out, accumulate):
+    """out (+)= dy2.sum(0): HIP row-chunk partials + column reduce (csrc/norms.hip) for bf16 row matrices."""
+    if (_BIAS_HIP and dy2.dtype == torch.bfloat16 and dy2.is_contiguous() and dy2.shape[1] % 8 == 0 and dy2.data_ptr() % 16 == 0
+            and out.dtype == torch.bfloat16 and out.is_contiguous()):
+        _lib().bias_grad_(dy2, out, accumulate)
+        return
+    s = dy2.sum(0, dtype=torch.float32)
+    if accumulate:
+        out.add_(s.to(out.dtype))
+    else:
+        out.copy_(s)
+
+
 # ---------------------------------------------------------------------------------------------------
 # linear
 # ---------------------------------------------------------------------------------------------------
@@ -128,13 +144,7 @@ class _Linear(Function):
         dw = _sink(w, lambda out, acc: _dw_into(dy2, x2, out, acc)) if ctx.needs_input_grad[1] else None
         db = None
         if ctx.has_b and ctx.needs_input_grad[2]:
-            def prod(out, acc):
-                s = dy2.sum(0, dtype=torch.float32)
-                if acc:
-                    out.add_(s.to(out.dtype))
-                else:
-                    out.copy_(s)
-            db = _sink(ctx.b, prod)
+            db = _sink(ctx.b, lambda out, acc: _bias_grad_into(dy2, out, acc))
         return dx, dw, db
 
 

@@ -311,3 +311,17 @@ def test_flash_attention_bwd_dq_variants(variant, D, Hq, Hkv, S, causal):
             assert rel_err(qkv.grad[:, lo:hi], x.grad[:, lo:hi]) < 3e-2
     finally:
         lib().flash_attn_set_dq_variant(old)
+
+
+@pytest.mark.parametrize("rows,H", [(8192, 768), (8192, 2304), (4096, 3072), (77, 24), (1000, 1024)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_bias_grad_matches_reference(rows, H, accumulate):
+    from kubeoperator_amd.ops import load
+
+    g = torch.Generator(device="cuda").manual_seed(rows + H)
+    dy = torch.randn(rows, H, device="cuda", generator=g).to(torch.bfloat16)
+    db = torch.randn(H, device="cuda", generator=g).to(torch.bfloat16)
+    ref = dy.float().sum(0) + (db.float() if accumulate else 0.0)
+    load().bias_grad_(dy, db, accumulate)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(db.float(), ref, atol=0.05 + 0.01 * ref.abs().max().item() / 10, rtol=1e-2)

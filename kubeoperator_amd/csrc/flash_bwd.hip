@@ -78,12 +78,15 @@ __device__ __forceinline__ int ds_slot(int key) {
   return (key & ~15) | (key & 3) | ((key & 4) << 1) | ((key & 8) >> 1);
 }
 
-template <int D, int NW, bool WDS = false>
+// DIRECT (no GQA, Hq == Hkv): the workgroup's sums are already the final dK / dV, written as bf16 straight
+// into dk_part / dv_part reinterpreted as the bf16 outputs (row strides dks / dvs), with no finalize pass.
+template <int D, int NW, bool WDS = false, bool DIRECT = false>
 __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ nlse, const float* __restrict__ ndelta,
     float* __restrict__ dk_part, float* __restrict__ dv_part, bf16_t* __restrict__ ds, int B, int S, int Hq,
-    int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t dos, float scale, int causal) {
+    int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t dos, float scale, int causal, int64_t dks = 0,
+    int64_t dvs = 0) {
   // LDS: the workgroup's K block (BN rows, read as the S = Q.K^T B operand) + a 2-deep ring of 32-query
   // stages {Q, dO, lse/delta}; 66 KiB at D = 128 so two workgroups share a CU (V^T stays in VGPRs).
   constexpr int BN = 32 * NW, BQ = 32, ROWB = D * 2;
@@ -266,6 +269,23 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
       });
     }
     asm volatile("" ::: "memory");
+  }
+  if constexpr (DIRECT) {
+    bf16_t* dkb = reinterpret_cast<bf16_t*>(dk_part) + (int64_t)(b * S + k0w + r) * dks + hq * D;
+    bf16_t* dvb = reinterpret_cast<bf16_t*>(dv_part) + (int64_t)(b * S + k0w + r) * dvs + hq * D;
+#pragma unroll
+    for (int dt = 0; dt < D / 32; ++dt) {
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = dt * 32 + 8 * g4 + 4 * hh;
+        *reinterpret_cast<u32x2*>(dkb + d) =
+            u32x2{pack2(dkacc[dt][4 * g4] * scale, dkacc[dt][4 * g4 + 1] * scale),
+                  pack2(dkacc[dt][4 * g4 + 2] * scale, dkacc[dt][4 * g4 + 3] * scale)};
+        *reinterpret_cast<u32x2*>(dvb + d) =
+            u32x2{pack2(dvacc[dt][4 * g4], dvacc[dt][4 * g4 + 1]), pack2(dvacc[dt][4 * g4 + 2], dvacc[dt][4 * g4 + 3])};
+      }
+    }
+    return;
   }
   // per-q-head partials: lane holds dK^T[d][key = k0w + r]
   float* dkp = dk_part + (int64_t)(b * S + k0w + r) * Hq * D + hq * D;
@@ -833,6 +853,8 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv);
     (void)hipFuncSetAttribute((const void*)fa_bwd_dkdv_kernel<D, NW, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv);
+    (void)hipFuncSetAttribute((const void*)fa_bwd_dkdv_kernel<D, NW, true, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_kv);
     (void)hipFuncSetAttribute((const void*)fa_bwd_dq_kernel<D, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds_q);
     attr = true;
@@ -840,15 +862,21 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
   const int variant = dq_variant();
   if (use_ds(B, S, Hq)) {
     bf16_t* ds = reinterpret_cast<bf16_t*>(ndelta + T * Hq);
-    fa_bwd_dkdv_kernel<D, NW, true><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(
-        q, k, v, dout, nlse, ndelta, dk_part, dv_part, ds, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);
+    const bool direct = Hq == Hkv;
+    if (direct)
+      fa_bwd_dkdv_kernel<D, NW, true, true><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(
+          q, k, v, dout, nlse, ndelta, reinterpret_cast<float*>(dk), reinterpret_cast<float*>(dv), ds, B, S, Hq, Hkv,
+          qs, ks, vs, dos, scale, causal, dks, dvs);
+    else
+      fa_bwd_dkdv_kernel<D, NW, true><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(
+          q, k, v, dout, nlse, ndelta, dk_part, dv_part, ds, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);
     const int grp = Hq / Hkv;  // heads per workgroup: largest power of two dividing the GQA group, <= 8
     const int hp = (grp % 8 == 0) ? 8 : (grp % 4 == 0) ? 4 : (grp % 2 == 0) ? 2 : 1;
     if (hp == 8) launch_dq_ds<D, 8>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
     else if (hp == 4) launch_dq_ds<D, 4>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
     else if (hp == 2) launch_dq_ds<D, 2>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
     else launch_dq_ds<D, 1>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-    fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs);
+    if (!direct) fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs);
     return;
   }
   fa_bwd_dkdv_kernel<D, NW, false><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(

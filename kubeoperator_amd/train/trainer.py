@@ -37,6 +37,7 @@ class TrainConfig:
     bucket_mb: int = 512
     overlap_optimizer: bool = True  # AdamW on its own stream, gated per bucket into the next forward
     transposed_weights: bool = True  # keep W^T copies of wide weights for the dX GEMMs (GPU only)
+    cuda_graph: bool = False  # replay each micro-batch's forward + backward as a captured HIP graph (1 GPU)
     seed: int = 1234
     model_overrides: dict = field(default_factory=dict)
 
@@ -76,6 +77,12 @@ class Trainer:
                               store=self.store if tc.overlap_optimizer else None,
                               on_segment=self.dp.publish_segment)
         self.step = 0
+        if tc.cuda_graph and (dev.type != "cuda" or info.world != 1):
+            raise ValueError("cuda_graph needs one GPU rank (collectives are not captured)")
+        self._graphs: dict = {}
+        self._graph_loss: dict = {}
+        self._graph_pool = None
+        self._static = None
         self.setup_seconds = time.time() - t0
 
     @property
@@ -87,9 +94,16 @@ class Trainer:
         """``batches``: iterable of ``grad_accum`` (ids, targets) pairs, each [micro_batch, seq_len]."""
         losses = []
         n = self.tc.grad_accum
+        graphed = self.tc.cuda_graph and self.step > 0  # step 0 runs eagerly: lazy library / workspace init
+        if graphed:
+            # the captured micro-batch reads no forward gate: join the optimizer stream once instead
+            self.store.await_all()
         for i, (ids, tgt) in enumerate(batches):
             self.store.begin_microbatch(i)
             self.dp.sync = i == n - 1
+            if graphed:
+                losses.append(self._replay(min(i, 1), ids, tgt))
+                continue
             loss = self.model(ids, tgt)
             loss.backward()
             losses.append(loss.detach())
@@ -100,6 +114,28 @@ class Trainer:
             self.store.refresh_transposed()
         self.step += 1
         return torch.stack(losses).mean()
+
+    # HIP graphs -----------------------------------------------------------------------------------
+    def _replay(self, key: int, ids, tgt) -> torch.Tensor:
+        """Forward + backward of one micro-batch as a captured HIP graph (``torch.cuda.CUDAGraph`` is a
+        hipGraph on ROCm): one launch for the ~40 kernels per layer, so small micro-batches stop being bound
+        by host-side launch and autograd overhead. Two graphs: ``key`` 0 overwrites the flat gradient buffer
+        (first micro-batch), ``key`` 1 accumulates into it. Inputs are copied into static buffers; the loss
+        is the graph's static output. Both graphs share one memory pool (they never run concurrently)."""
+        if self._static is None:
+            self._static = (torch.empty_like(ids), torch.empty_like(tgt))
+        if key not in self._graphs:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=self._graph_pool):
+                loss = self.model(*self._static)
+                loss.backward()
+            self._graph_pool = g.pool()
+            self._graphs[key] = g
+            self._graph_loss[key] = loss.detach()
+        self._static[0].copy_(ids)
+        self._static[1].copy_(tgt)
+        self._graphs[key].replay()
+        return self._graph_loss[key].clone()
 
     # checkpoint -----------------------------------------------------------------------------------
     def state_dict(self):

@@ -142,6 +142,18 @@ Tensor swiglu_bwd(const Tensor& gu, const Tensor& dh) {
   rc(kop::swiglu_bwd(bp(gu), bp(dh), bp(dgu), T, (int)F, cur_stream()), "swiglu_bwd");
   return dgu;
 }
+std::vector<Tensor> swiglu_bwd_t(const Tensor& gu, const Tensor& dh) {
+  check_bf16(gu, "gate_up");
+  check_bf16(dh, "dh");
+  TORCH_CHECK(gu.is_contiguous() && dh.is_contiguous(), "swiglu_bwd_t inputs must be contiguous");
+  const int64_t F = gu.size(-1) / 2;
+  const int64_t T = gu.numel() / (2 * F);
+  auto dgu = at::empty_like(gu);
+  auto dgut = at::empty({2 * F, T}, gu.options());
+  rc(kop::swiglu_bwd_t(bp(gu), bp(dh), bp(dgu), bp(dgut), T, (int)F, cur_stream()),
+     "swiglu_bwd_t (tokens and F must be multiples of 64)");
+  return {dgu, dgut};
+}
 Tensor gelu_fwd(const Tensor& x) {
   check_bf16(x, "x");
   TORCH_CHECK(x.is_contiguous(), "x must be contiguous");
@@ -274,6 +286,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("rope_", &rope_);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("swiglu_bwd_t", &swiglu_bwd_t);
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("cross_entropy_fwd_", &cross_entropy_fwd_);

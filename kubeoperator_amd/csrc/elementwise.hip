@@ -128,6 +128,84 @@ int swiglu_bwd(const bf16_t* gu, const bf16_t* dh, bf16_t* dgu, int64_t T, int F
   return 0;
 }
 
+// SwiGLU backward that also writes dgu^T ([2F, T]), the K-contiguous operand of the gate/up weight-gradient
+// GEMM: one 64-token x 64-column tile of gate and of up per workgroup, dg / du computed in registers, stored
+// row-major and staged through LDS (pitch 33 dwords, conflict-free column reads as in csrc/transpose.hip) for
+// the transposed stores. Replaces swiglu_bwd + a separate transpose of dgu (one read + one write of 2*T*F
+// bf16 saved). Row tiles fastest in the grid (adjacent transposed output segments).
+__global__ void __launch_bounds__(256) swiglu_bwd_t_kernel(const bf16_t* __restrict__ gu, const bf16_t* __restrict__ dh,
+                                                           bf16_t* __restrict__ dgu, bf16_t* __restrict__ dgut,
+                                                           int64_t T, int F, int64_t tiles_r) {
+  constexpr int P = 33;
+  __shared__ uint32_t lg[64 * P], lu[64 * P];
+  const int t = threadIdx.x;
+  const int64_t tr = blockIdx.x % tiles_r, tc = blockIdx.x / tiles_r;
+  const int64_t r0 = tr * 64;
+  const int c0 = (int)tc * 64;
+  u32x4 gv[2], uv[2], dv[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int64_t row = r0 + p * 32 + (t >> 3);
+    const int col = c0 + (t & 7) * 8;
+    gv[p] = *reinterpret_cast<const u32x4*>(gu + row * 2 * F + col);
+    uv[p] = *reinterpret_cast<const u32x4*>(gu + row * 2 * F + F + col);
+    dv[p] = *reinterpret_cast<const u32x4*>(dh + row * F + col);
+  }
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int lrow = p * 32 + (t >> 3), ch = t & 7;
+    const int64_t row = r0 + lrow;
+    const int col = c0 + ch * 8;
+    float g[8], u[8], d[8], dg[8], du[8];
+    unpack8(gv[p], g);
+    unpack8(uv[p], u);
+    unpack8(dv[p], d);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float sg = sigmoidf_fast(g[i]);
+      const float silu = g[i] * sg;
+      du[i] = d[i] * silu;
+      dg[i] = d[i] * u[i] * sg * (1.f + g[i] * (1.f - sg));
+    }
+    const u32x4 pg = pack8(dg), pu = pack8(du);
+    *reinterpret_cast<u32x4*>(dgu + row * 2 * F + col) = pg;
+    *reinterpret_cast<u32x4*>(dgu + row * 2 * F + F + col) = pu;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      lg[lrow * P + ch * 4 + i] = pg[i];
+      lu[lrow * P + ch * 4 + i] = pu[i];
+    }
+  }
+  __syncthreads();
+  const int chunk = t & 7, pair = t >> 3;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const uint32_t* L = half ? lu : lg;
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = L[(chunk * 8 + i) * P + pair];
+    u32x4 lo, hi;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      lo[i] = (w[2 * i] & 0xffffu) | (w[2 * i + 1] << 16);
+      hi[i] = (w[2 * i] >> 16) | (w[2 * i + 1] & 0xffff0000u);
+    }
+    const int64_t oc = (int64_t)half * F + c0 + 2 * pair, orr = r0 + chunk * 8;
+    *reinterpret_cast<u32x4*>(dgut + oc * T + orr) = lo;
+    *reinterpret_cast<u32x4*>(dgut + (oc + 1) * T + orr) = hi;
+  }
+}
+
+int swiglu_bwd_t(const bf16_t* gu, const bf16_t* dh, bf16_t* dgu, bf16_t* dgut, int64_t T, int F,
+                 hipStream_t stream) {
+  if (F % 64 || T % 64) return -1;
+  if (T == 0) return 0;
+  const int64_t tiles_r = T / 64, n = tiles_r * (F / 64);
+  if (n > 0x7fffffff) return -2;
+  swiglu_bwd_t_kernel<<<(unsigned)n, 256, 0, stream>>>(gu, dh, dgu, dgut, T, F, tiles_r);
+  return 0;
+}
+
 // ---------------------------------------------------------------------------------------------
 // GELU (tanh approximation, GPT-2): y = 0.5 x (1 + tanh(k (x + 0.044715 x^3))), k = sqrt(2/pi)
 // ---------------------------------------------------------------------------------------------

@@ -251,6 +251,52 @@ def swiglu(gu):
     return _SwiGLU.apply(gu)
 
 
+_SWIGLU_T = os.environ.get("KOP_SWIGLU_T", "1") != "0"
+
+
+class _LinearSwiGLU(Function):
+    """h = swiglu(x . W_gu^T) as one autograd node, so the backward can take dgu^T (the K-contiguous operand
+    of the weight-gradient GEMM) from the SwiGLU backward kernel itself instead of transposing dgu afterwards
+    (``swiglu_bwd_t``: one read + one write of the [T, 2F] gradient saved per layer and micro-batch)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        x2 = x.reshape(-1, x.shape[-1])
+        gu = torch.mm(x2, w.t())
+        ctx.save_for_backward(x2, w, gu)
+        ctx.in_shape = x.shape
+        h = _lib().swiglu_fwd(gu)
+        return h.view(*x.shape[:-1], h.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dh):
+        x2, w, gu = ctx.saved_tensors
+        dh2 = dh.reshape(-1, gu.shape[1] // 2).contiguous()
+        T, F2 = gu.shape
+        fused_t = _SWIGLU_T and ((_DW_LAYOUT == "tn" or (_DW_LAYOUT == "auto" and min(F2, x2.shape[1]) >= _DW_TN_MIN_WIDTH))
+                   and T >= _DW_TN_MIN_ROWS and T % 64 == 0 and (F2 // 2) % 64 == 0 and _rows_ok(x2))
+        if fused_t:
+            dgu, dgut = _lib().swiglu_bwd_t(gu, dh2)
+        else:
+            dgu, dgut = _lib().swiglu_bwd(gu, dh2), None
+        dx = _dx(dgu, w).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            if dgut is not None:
+                dw = _sink(w, lambda out, acc: _mm_into(dgut, transpose(x2).t(), out, acc))
+            else:
+                dw = _sink(w, lambda out, acc: _dw_into(dgu, x2, out, acc))
+        return dx, dw
+
+
+def linear_swiglu(x, w):
+    """swiglu(linear(x, w)) with w = [gate | up] stacked on the output dimension."""
+    if not x.is_cuda:
+        return swiglu(F.linear(x, w))
+    _gate(w)
+    return _LinearSwiGLU.apply(x, w)
+
+
 class _GELU(Function):
     @staticmethod
     def forward(ctx, x):

@@ -325,3 +325,41 @@ def test_bias_grad_matches_reference(rows, H, accumulate):
     load().bias_grad_(dy, db, accumulate)
     torch.cuda.synchronize()
     torch.testing.assert_close(db.float(), ref, atol=0.05 + 0.01 * ref.abs().max().item() / 10, rtol=1e-2)
+
+
+@pytest.mark.parametrize("T,F", [(256, 128), (1024, 448)])
+def test_swiglu_bwd_transposed_matches(T, F):
+    """swiglu_bwd_t = swiglu_bwd plus the exact transpose of its output."""
+    from kubeoperator_amd.ops import load
+
+    lib = load()
+    torch.manual_seed(3)
+    gu = torch.randn(T, 2 * F, device=DEV).to(torch.bfloat16)
+    dh = torch.randn(T, F, device=DEV).to(torch.bfloat16)
+    ref = lib.swiglu_bwd(gu, dh)
+    dgu, dgut = lib.swiglu_bwd_t(gu, dh)
+    assert torch.equal(dgu, ref)
+    assert dgut.shape == (2 * F, T) and torch.equal(dgut, ref.t())
+
+
+@pytest.mark.parametrize("layout", ["tn", "nt"])
+def test_linear_swiglu_matches_separate_ops(layout, monkeypatch):
+    """The fused gate/up projection + SwiGLU node gives the same output and gradients as linear -> swiglu."""
+    import kubeoperator_amd.ops.functional as kf
+
+    monkeypatch.setattr(kf, "_DW_LAYOUT", layout)
+    torch.manual_seed(5)
+    T, H, F = 1024, 256, 320
+    x = torch.randn(T, H, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    w = (0.05 * torch.randn(2 * F, H, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    dh = torch.randn(T, F, device=DEV).to(torch.bfloat16)
+    h1 = kf.linear_swiglu(x, w)
+    h1.backward(dh)
+    gx1, gw1 = x.grad.clone(), w.grad.clone()
+    x.grad = None
+    w.grad = None
+    h2 = kf.swiglu(kf.linear(x, w))
+    h2.backward(dh)
+    assert torch.equal(h1, h2)
+    assert torch.equal(gx1, x.grad)
+    assert rel_err(gw1, w.grad) < 1e-2

@@ -142,6 +142,17 @@ Tensor swiglu_bwd(const Tensor& gu, const Tensor& dh) {
   rc(kop::swiglu_bwd(bp(gu), bp(dh), bp(dgu), T, (int)F, cur_stream()), "swiglu_bwd");
   return dgu;
 }
+std::vector<Tensor> swiglu_fwd_t(const Tensor& gu) {
+  check_bf16(gu, "gate_up");
+  TORCH_CHECK(gu.is_contiguous(), "gate_up must be contiguous");
+  const int64_t F = gu.size(-1) / 2;
+  const int64_t T = gu.numel() / (2 * F);
+  auto h = at::empty({T, F}, gu.options());
+  auto ht = at::empty({F, T}, gu.options());
+  rc(kop::swiglu_fwd_t(bp(gu), bp(h), bp(ht), T, (int)F, cur_stream()),
+     "swiglu_fwd_t (tokens and F must be multiples of 64)");
+  return {h, ht};
+}
 std::vector<Tensor> swiglu_bwd_t(const Tensor& gu, const Tensor& dh) {
   check_bf16(gu, "gate_up");
   check_bf16(dh, "dh");
@@ -287,6 +298,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("swiglu_bwd_t", &swiglu_bwd_t);
+  m.def("swiglu_fwd_t", &swiglu_fwd_t);
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("cross_entropy_fwd_", &cross_entropy_fwd_);

@@ -128,6 +128,63 @@ int swiglu_bwd(const bf16_t* gu, const bf16_t* dh, bf16_t* dgu, int64_t T, int F
   return 0;
 }
 
+// SwiGLU forward that also writes h^T ([F, T]): the down projection's weight gradient dW = dY^T h then runs
+// in the K-contiguous layout from the saved h^T (the row-major h feeds the forward GEMM and is not kept).
+// Same tiling as swiglu_bwd_t_kernel.
+__global__ void __launch_bounds__(256) swiglu_fwd_t_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ h,
+                                                           bf16_t* __restrict__ ht, int64_t T, int F, int64_t tiles_r) {
+  constexpr int P = 33;
+  __shared__ uint32_t lh[64 * P];
+  const int t = threadIdx.x;
+  const int64_t tr = blockIdx.x % tiles_r, tc = blockIdx.x / tiles_r;
+  const int64_t r0 = tr * 64;
+  const int c0 = (int)tc * 64;
+  u32x4 gv[2], uv[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int64_t row = r0 + p * 32 + (t >> 3);
+    const int col = c0 + (t & 7) * 8;
+    gv[p] = *reinterpret_cast<const u32x4*>(gu + row * 2 * F + col);
+    uv[p] = *reinterpret_cast<const u32x4*>(gu + row * 2 * F + F + col);
+  }
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int lrow = p * 32 + (t >> 3), ch = t & 7;
+    float g[8], u[8], o[8];
+    unpack8(gv[p], g);
+    unpack8(uv[p], u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = g[i] * sigmoidf_fast(g[i]) * u[i];
+    const u32x4 po = pack8(o);
+    *reinterpret_cast<u32x4*>(h + (r0 + lrow) * F + c0 + ch * 8) = po;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) lh[lrow * P + ch * 4 + i] = po[i];
+  }
+  __syncthreads();
+  const int chunk = t & 7, pair = t >> 3;
+  uint32_t w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = lh[(chunk * 8 + i) * P + pair];
+  u32x4 lo, hi;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    lo[i] = (w[2 * i] & 0xffffu) | (w[2 * i + 1] << 16);
+    hi[i] = (w[2 * i] >> 16) | (w[2 * i + 1] & 0xffff0000u);
+  }
+  const int64_t oc = c0 + 2 * pair, orr = r0 + chunk * 8;
+  *reinterpret_cast<u32x4*>(ht + oc * T + orr) = lo;
+  *reinterpret_cast<u32x4*>(ht + (oc + 1) * T + orr) = hi;
+}
+
+int swiglu_fwd_t(const bf16_t* gu, bf16_t* h, bf16_t* ht, int64_t T, int F, hipStream_t stream) {
+  if (F % 64 || T % 64) return -1;
+  if (T == 0) return 0;
+  const int64_t tiles_r = T / 64, n = tiles_r * (F / 64);
+  if (n > 0x7fffffff) return -2;
+  swiglu_fwd_t_kernel<<<(unsigned)n, 256, 0, stream>>>(gu, h, ht, T, F, tiles_r);
+  return 0;
+}
+
 // SwiGLU backward that also writes dgu^T ([2F, T]), the K-contiguous operand of the gate/up weight-gradient
 // GEMM: one 64-token x 64-column tile of gate and of up per workgroup, dg / du computed in registers, stored
 // row-major and staged through LDS (pitch 33 dwords, conflict-free column reads as in csrc/transpose.hip) for

@@ -24,6 +24,7 @@ int rope_inplace(bf16_t* x, const float* cos_t, const float* sin_t, const int* p
                  int D, int64_t row_stride, bool inverse, hipStream_t stream);
 int swiglu_fwd(const bf16_t* gu, bf16_t* h, int64_t T, int F, hipStream_t stream);
 int swiglu_bwd(const bf16_t* gu, const bf16_t* dh, bf16_t* dgu, int64_t T, int F, hipStream_t stream);
+int swiglu_fwd_t(const bf16_t* gu, bf16_t* h, bf16_t* ht, int64_t T, int F, hipStream_t stream);
 int swiglu_bwd_t(const bf16_t* gu, const bf16_t* dh, bf16_t* dgu, bf16_t* dgut, int64_t T, int F, hipStream_t stream);
 int gelu_fwd(const bf16_t* x, bf16_t* y, int64_t n, hipStream_t stream);
 int gelu_bwd(const bf16_t* x, const bf16_t* dy, bf16_t* dx, int64_t n, hipStream_t stream);

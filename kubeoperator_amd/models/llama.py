@@ -50,8 +50,7 @@ class LlamaBlock(nn.Module):
         a = kf.rope_attention(qkv, cos, sin, B, S, c.n_heads, c.n_kv_heads, c.head_dim, causal=True)
         a = kf.linear(a, self.wo)
         y2, x2 = kf.rms_norm(x1, self.mlp_norm, c.norm_eps, residual=a)
-        h = kf.linear_swiglu(y2, self.w_gate_up)
-        return x2, kf.linear(h, self.w_down)
+        return x2, kf.swiglu_mlp(y2, self.w_gate_up, self.w_down)
 
 
 class Llama(nn.Module):

@@ -297,6 +297,74 @@ def linear_swiglu(x, w):
     return _LinearSwiGLU.apply(x, w)
 
 
+
+def _tn_ok(T: int, F2: int, H: int) -> bool:
+    """Weight gradient of a [T] x [F2, H] projection through transposed operands (see _dw_into)."""
+    return ((_DW_LAYOUT == "tn" or (_DW_LAYOUT == "auto" and min(F2, H) >= _DW_TN_MIN_WIDTH))
+            and T >= _DW_TN_MIN_ROWS and T % 64 == 0)
+
+
+class _SwiGLUMLP(Function):
+    """y = swiglu(x . W_gu^T) . W_d^T as one autograd node. With the transposed weight-gradient layout the
+    SwiGLU kernels also emit the K-contiguous operands of both weight-gradient GEMMs: the forward writes h^T
+    (saved INSTEAD of h: the down projection's backward only needs h for dW_d) and the backward writes dgu^T,
+    so neither h nor dgu is transposed separately."""
+
+    @staticmethod
+    def forward(ctx, x, w_gu, w_d):
+        lib = _lib()
+        x2 = x.reshape(-1, x.shape[-1])
+        gu = torch.mm(x2, w_gu.t())
+        T, F2 = gu.shape
+        F = F2 // 2
+        ht = None
+        if _SWIGLU_T and F % 64 == 0 and _tn_ok(T, w_d.shape[0], F):
+            h, ht = lib.swiglu_fwd_t(gu)
+        else:
+            h = lib.swiglu_fwd(gu)
+        y = torch.mm(h, w_d.t())
+        ctx.save_for_backward(x2, w_gu, w_d, gu, ht if ht is not None else h)
+        ctx.has_ht = ht is not None
+        ctx.in_shape = x.shape
+        return y.view(*x.shape[:-1], w_d.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _lib()
+        x2, w_gu, w_d, gu, h_or_ht = ctx.saved_tensors
+        T, F2 = gu.shape
+        dy2 = dy.reshape(-1, w_d.shape[0])
+        dh = _dx(dy2, w_d)
+        dw_d = None
+        if ctx.needs_input_grad[2]:
+            if ctx.has_ht:
+                a = transpose(dy2) if _rows_ok(dy2) else dy2.t()
+                dw_d = _sink(w_d, lambda out, acc: _mm_into(a, h_or_ht.t(), out, acc))
+            else:
+                dw_d = _sink(w_d, lambda out, acc: _dw_into(dy2, h_or_ht, out, acc))
+        dh = dh.contiguous()
+        if _SWIGLU_T and (F2 // 2) % 64 == 0 and _tn_ok(T, F2, x2.shape[1]) and _rows_ok(x2):
+            dgu, dgut = lib.swiglu_bwd_t(gu, dh)
+        else:
+            dgu, dgut = lib.swiglu_bwd(gu, dh), None
+        dx = _dx(dgu, w_gu).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
+        dw_gu = None
+        if ctx.needs_input_grad[1]:
+            if dgut is not None:
+                dw_gu = _sink(w_gu, lambda out, acc: _mm_into(dgut, transpose(x2).t(), out, acc))
+            else:
+                dw_gu = _sink(w_gu, lambda out, acc: _dw_into(dgu, x2, out, acc))
+        return dx, dw_gu, dw_d
+
+
+def swiglu_mlp(x, w_gu, w_d):
+    """linear(swiglu(linear(x, w_gu)), w_d): the Llama MLP (w_gu = [gate | up] on the output dimension)."""
+    if not x.is_cuda:
+        return F.linear(swiglu(F.linear(x, w_gu)), w_d)
+    _gate(w_gu, w_d)
+    return _SwiGLUMLP.apply(x, w_gu, w_d)
+
+
 class _GELU(Function):
     @staticmethod
     def forward(ctx, x):

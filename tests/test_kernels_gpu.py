@@ -363,3 +363,37 @@ def test_linear_swiglu_matches_separate_ops(layout, monkeypatch):
     assert torch.equal(h1, h2)
     assert torch.equal(gx1, x.grad)
     assert rel_err(gw1, w.grad) < 1e-2
+
+
+def test_swiglu_fwd_transposed_matches():
+    from kubeoperator_amd.ops import load
+
+    lib = load()
+    torch.manual_seed(4)
+    gu = torch.randn(512, 2 * 192, device=DEV).to(torch.bfloat16)
+    h, ht = lib.swiglu_fwd_t(gu)
+    assert torch.equal(h, lib.swiglu_fwd(gu)) and torch.equal(ht, h.t())
+
+
+@pytest.mark.parametrize("layout", ["tn", "nt"])
+def test_swiglu_mlp_matches_separate_ops(layout, monkeypatch):
+    """The fused MLP node (h^T saved, dgu^T from the SwiGLU backward) matches linear -> swiglu -> linear."""
+    import kubeoperator_amd.ops.functional as kf
+
+    monkeypatch.setattr(kf, "_DW_LAYOUT", layout)
+    torch.manual_seed(6)
+    T, H, F = 1024, 256, 320
+    x = torch.randn(T, H, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    wgu = (0.05 * torch.randn(2 * F, H, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    wd = (0.05 * torch.randn(H, F, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    dy = torch.randn(T, H, device=DEV).to(torch.bfloat16)
+    y1 = kf.swiglu_mlp(x, wgu, wd)
+    y1.backward(dy)
+    g1 = [t.grad.clone() for t in (x, wgu, wd)]
+    for t in (x, wgu, wd):
+        t.grad = None
+    y2 = kf.linear(kf.swiglu(kf.linear(x, wgu)), wd)
+    y2.backward(dy)
+    assert torch.equal(y1, y2)
+    for a, b in zip(g1, (x.grad, wgu.grad, wd.grad)):
+        assert rel_err(a, b) < 1e-2

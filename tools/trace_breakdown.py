@@ -18,9 +18,9 @@ GROUPS = [
     ("attn_fwd", re.compile(r"fa_fwd")),
     ("attn_bwd", re.compile(r"fa_bwd")),
     ("adamw", re.compile(r"adamw")),
-    ("transpose", re.compile(r"transpose_kernel")),
+    ("transpose", re.compile(r"transpose_(wide_)?kernel")),
     ("norm", re.compile(r"norm_|col_reduce")),
-    ("swiglu/gelu", re.compile(r"swiglu|gelu")),
+    ("swiglu/gelu", re.compile(r"swiglu|gelu")),  # incl. the fused transposed-output forms
     ("rope", re.compile(r"rope")),
     ("cross_entropy", re.compile(r"\bce_|cross_entropy|xent")),
     ("grad_norm", re.compile(r"sumsq|grad_norm")),

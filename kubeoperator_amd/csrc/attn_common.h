@@ -98,6 +98,18 @@ __device__ __forceinline__ float sum32(const f32x16& a, const f32x16& b) {
   const f2 s = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   return s[0] + s[1];
 }
+// s = s * c + b over one accumulator with packed FMAs (v_pk_fma_f32: two values per issue, half the VALU
+// slots of 16 v_fma_f32 in the softmax's exponent argument)
+__device__ __forceinline__ void fma_pk16(f32x16& s, float c, float b) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 c2 = {c, c}, b2 = {b, b};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const f2 t = __builtin_elementwise_fma(f2{s[2 * i], s[2 * i + 1]}, c2, b2);
+    s[2 * i] = t[0];
+    s[2 * i + 1] = t[1];
+  }
+}
 // accumulator registers 8h .. 8h+7 -> one bf16x8 MFMA operand (4 v_cvt_pk_bf16_f32, no sub-word moves)
 __device__ __forceinline__ bf16x8 pack_acc8(const f32x16& s, int h) {
   const u32x4 w = {pack2(s[8 * h], s[8 * h + 1]), pack2(s[8 * h + 2], s[8 * h + 3]), pack2(s[8 * h + 4], s[8 * h + 5]),

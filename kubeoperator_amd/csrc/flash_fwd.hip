@@ -216,7 +216,7 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_fwd_kernel(const bf16_t* __rest
 //     passed the barrier that follows its last read);
 //   * V^T fragments for the next 32-column block are read (ds_read_b64_tr_b16) while the current block's
 //     MFMAs run, retired by counted lgkmcnt waits; the first block's reads fly under the softmax.
-template <int D, bool STAGGER>
+template <int D, bool STAGGER, bool PK>
 __global__ void __launch_bounds__(512, 1) fa_fwd8_kernel(const bf16_t* __restrict__ q, const bf16_t* __restrict__ k,
                                                          const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
                                                          float* __restrict__ lse, int B, int S, int Hq, int Hkv,
@@ -358,10 +358,20 @@ __global__ void __launch_bounds__(512, 1) fa_fwd8_kernel(const bf16_t* __restric
 #pragma unroll
       for (int i = 0; i < DT; ++i) oacc[i] *= alpha;
     }
+    if constexpr (PK) {
+      fma_pk16(s0, scale_log2, -m);
+      fma_pk16(s1, scale_log2, -m);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      s0[j] = __builtin_amdgcn_exp2f(fmaf(s0[j], scale_log2, -m));
-      s1[j] = __builtin_amdgcn_exp2f(fmaf(s1[j], scale_log2, -m));
+      for (int j = 0; j < 16; ++j) {
+        s0[j] = __builtin_amdgcn_exp2f(s0[j]);
+        s1[j] = __builtin_amdgcn_exp2f(s1[j]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        s0[j] = __builtin_amdgcn_exp2f(fmaf(s0[j], scale_log2, -m));
+        s1[j] = __builtin_amdgcn_exp2f(fmaf(s1[j], scale_log2, -m));
+      }
     }
     l += sum32(s0, s1);
     const bf16x8 pf[4] = {pack_acc8(s0, 0), pack_acc8(s0, 1), pack_acc8(s1, 0), pack_acc8(s1, 1)};
@@ -442,19 +452,19 @@ __global__ void __launch_bounds__(512, 1) fa_fwd8_kernel(const bf16_t* __restric
   }
 }
 
-template <int D, bool STAGGER>
+template <int D, bool STAGGER, bool PK = false>
 static void launch_fwd8(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int S,
                         int Hq, int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t os, float sl2, bool causal,
                         hipStream_t stream) {
   const size_t lds = (STAGGER ? 4 : 3) * 2 * 64 * (D * 2);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)fa_fwd8_kernel<D, STAGGER>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)fa_fwd8_kernel<D, STAGGER, PK>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)lds);
     attr = true;
   }
   const int grid = B * Hq * (S / 256);
-  fa_fwd8_kernel<D, STAGGER><<<grid, 512, lds, stream>>>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal);
+  fa_fwd8_kernel<D, STAGGER, PK><<<grid, 512, lds, stream>>>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal);
 }
 
 constexpr int kFwdWaves = 4;
@@ -482,14 +492,16 @@ int flash_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o,
   const float sl2 = scale * 1.4426950408889634f;
   static const int variant = [] {
     const char* e = getenv("KOP_FWD_VARIANT");
-    return e ? atoi(e) : 8;
+    return e ? atoi(e) : 10;  // 10: lockstep 8-wave kernel with packed-FMA softmax (8: unpacked, 9: staggered)
   }();
   if (S % 256 == 0 && variant >= 8) {
     if (D == 128) {
       if (variant == 9) launch_fwd8<128, true>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
+      else if (variant == 10) launch_fwd8<128, false, true>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
       else launch_fwd8<128, false>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
     } else if (D == 64) {
       if (variant == 9) launch_fwd8<64, true>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
+      else if (variant == 10) launch_fwd8<64, false, true>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
       else launch_fwd8<64, false>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
     } else return -3;
     return 0;

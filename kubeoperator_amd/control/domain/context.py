@@ -31,7 +31,13 @@ def transport() -> Transport:
         fn = _transport_factory
     if fn is not None:
         return fn()
-    return make_transport(get_config()["DEFAULT_TRANSPORT"])
+    cfg = get_config()
+    kind = cfg["DEFAULT_TRANSPORT"]
+    if kind == "ssh":  # host keys pinned per host under DATA_DIR (survive restarts of the control plane)
+        import os
+
+        return make_transport(kind, known_hosts_dir=os.path.join(cfg["DATA_DIR"], "ssh", "known_hosts"))
+    return make_transport(kind)
 
 
 def enc(value: str) -> str:

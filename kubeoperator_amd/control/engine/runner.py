@@ -34,7 +34,7 @@ import yaml
 
 from .inventory import Inventory
 from .modules import MODULES, ModuleContext, ModuleError
-from .templating import TemplateError, evaluate, render
+from .templating import LazyVars, TemplateError, evaluate, render
 from .transport import FakeTransport, HostConn, Transport, Unreachable
 
 TASK_KEYWORDS = {
@@ -240,7 +240,8 @@ class _HostVars(dict):
         self._r = runner
 
     def __getitem__(self, host):
-        return self._r.base_vars(host)
+        # inventory + facts + extra vars (as Ansible's HostVars); templated values render on lookup
+        return LazyVars({**self._r.base_vars(host), **self._r.extra_vars})
 
     def __contains__(self, host):
         return host in self._r.inventory.hosts

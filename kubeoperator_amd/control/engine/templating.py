@@ -2,7 +2,8 @@
 
 Recursive templating of strings inside dicts/lists, "naked" conditional evaluation for ``when`` /
 ``failed_when`` / ``changed_when`` / ``until``, lazily templated variables (a var whose value is itself a
-template is resolved on use, like Ansible's HostVars), and filters: default/d, bool, int, float, string,
+template is resolved on use through a custom Jinja context, like Ansible's HostVars; recursion is bounded),
+a sandboxed environment (API-supplied config values cannot reach Python internals), and filters: default/d, bool, int, float, string,
 lower/upper, length/count, join, split, replace, regex_replace, regex_search, to_json/from_json,
 to_yaml/from_yaml, to_nice_yaml, b64encode/b64decode, basename/dirname, ipaddr (address / network /
 netmask / prefix / nth host), unique, union, difference, intersect, first/last, min/max, mandatory,
@@ -16,11 +17,14 @@ import json
 import os
 import re
 import shlex
+import threading
 
 import jinja2
 import yaml
 from jinja2 import StrictUndefined
-from jinja2.nativetypes import NativeEnvironment
+from jinja2.nativetypes import NativeCodeGenerator, NativeTemplate, native_concat
+from jinja2.runtime import Context, missing
+from jinja2.sandbox import ImmutableSandboxedEnvironment, SecurityError
 
 
 class TemplateError(Exception):
@@ -165,14 +169,89 @@ TESTS = {
 }
 
 
-class _Undef(jinja2.ChainableUndefined):
+class TemplateRecursionError(TemplateError):
     pass
 
 
+_MAX_DEPTH = 16
+_tls = threading.local()
+
+
+def _expand(value, root):
+    """Resolve a variable's value on use: a string that is itself a template is rendered against ``root``
+    (Ansible templates variables lazily, so role defaults may reference inventory / extra vars), and a dict
+    is wrapped so its templated members resolve the same way when they are looked up."""
+    if isinstance(value, str):
+        if not has_template(value):
+            return value
+        depth = getattr(_tls, "depth", 0)
+        if depth >= _MAX_DEPTH:
+            raise TemplateRecursionError(f"recursive loop detected in template string: {value!r}")
+        _tls.depth = depth + 1
+        try:
+            return render(value, root)
+        finally:
+            _tls.depth = depth
+    if type(value) is dict:
+        return _BoundVars(value, root)
+    if isinstance(value, list) and any(has_template(x) for x in value):
+        return [_expand(x, root) for x in value]
+    return value
+
+
+class _BoundVars(dict):
+    """A dict-valued variable whose templated members render against the enclosing variable set."""
+
+    def __init__(self, base: dict, root):
+        super().__init__(base)
+        self._root = root
+
+    def __getitem__(self, key):
+        return _expand(super().__getitem__(key), self._root)
+
+    def get(self, key, default=None):
+        return self[key] if key in self else default
+
+    def items(self):
+        return [(k, self[k]) for k in self.keys()]
+
+    def values(self):
+        return [self[k] for k in self.keys()]
+
+
+class LazyVars(_BoundVars):
+    """A variable set (e.g. one host's ``hostvars`` entry) whose templated values render against itself."""
+
+    def __init__(self, base: dict):
+        super().__init__(base, None)
+        self._root = self
+
+
+class _LazyContext(Context):
+    def resolve_or_missing(self, key):
+        v = super().resolve_or_missing(key)
+        if v is missing:
+            return v
+        return _expand(v, self.parent)
+
+
+class _SandboxedNativeEnvironment(ImmutableSandboxedEnvironment):
+    """Sandboxed environment whose single-expression renders keep their Python type."""
+
+    code_generator_class = NativeCodeGenerator
+    concat = staticmethod(native_concat)
+
+
+_SandboxedNativeEnvironment.template_class = NativeTemplate
+
+
 def _make_env(native: bool):
-    cls = NativeEnvironment if native else jinja2.Environment
+    # Sandboxed: cluster configs and execution params come from API users (item MANAGERs) and are merged
+    # into the variables, so a template must not reach Python internals (attribute walks to globals, etc.).
+    cls = _SandboxedNativeEnvironment if native else ImmutableSandboxedEnvironment
     env = cls(undefined=StrictUndefined, keep_trailing_newline=True, trim_blocks=True, lstrip_blocks=False,
               extensions=["jinja2.ext.do", "jinja2.ext.loopcontrols"])
+    env.context_class = _LazyContext
     env.filters.update(FILTERS)
     env.tests.update(TESTS)
     return env
@@ -182,18 +261,8 @@ _ENV_STR = _make_env(False)
 _ENV_NATIVE = _make_env(True)
 
 
-class VarView(dict):
-    """Variable mapping whose string values that are templates are rendered lazily on access."""
-
-    def __init__(self, base: dict, depth: int = 0):
-        super().__init__(base)
-        self._depth = depth
-
-    def __getitem__(self, key):
-        v = super().__getitem__(key)
-        if isinstance(v, str) and ("{{" in v or "{%" in v) and self._depth < 16:
-            return render(v, VarView(dict(self), self._depth + 1))
-        return v
+def _plain(variables) -> dict:
+    return variables if isinstance(variables, dict) else dict(variables)
 
 
 def has_template(s) -> bool:
@@ -205,13 +274,17 @@ def render(value, variables: dict):
     if isinstance(value, str):
         if not has_template(value):
             return value
-        ctx = variables if isinstance(variables, VarView) else VarView(variables)
+        ctx = _plain(variables)
         stripped = value.strip()
         try:
             if stripped.startswith("{{") and stripped.endswith("}}") and stripped.count("{{") == 1:
                 out = _ENV_NATIVE.from_string(stripped).render(ctx)
                 return out
             return _ENV_STR.from_string(value).render(ctx)
+        except TemplateError:
+            raise
+        except SecurityError as e:
+            raise TemplateError(f"unsafe template {value!r}: {e}") from e
         except jinja2.UndefinedError as e:
             raise TemplateError(f"undefined variable in {value!r}: {e}") from e
         except jinja2.TemplateError as e:
@@ -225,9 +298,12 @@ def render(value, variables: dict):
 
 def render_text(text: str, variables: dict) -> str:
     """Template a whole file (the ``template`` module); always returns text."""
-    ctx = variables if isinstance(variables, VarView) else VarView(variables)
     try:
-        return _ENV_STR.from_string(text).render(ctx)
+        return _ENV_STR.from_string(text).render(_plain(variables))
+    except TemplateError:
+        raise
+    except SecurityError as e:
+        raise TemplateError(f"unsafe template: {e}") from e
     except jinja2.UndefinedError as e:
         raise TemplateError(f"undefined variable in template: {e}") from e
     except jinja2.TemplateError as e:
@@ -247,9 +323,12 @@ def evaluate(cond, variables: dict) -> bool:
     expr = str(cond).strip()
     if has_template(expr) and expr.startswith("{{") and expr.endswith("}}"):
         expr = expr[2:-2]
-    ctx = variables if isinstance(variables, VarView) else VarView(variables)
     try:
-        out = _ENV_NATIVE.from_string("{{ (" + expr + ") }}").render(ctx)
+        out = _ENV_NATIVE.from_string("{{ (" + expr + ") }}").render(_plain(variables))
+    except TemplateError:
+        raise
+    except SecurityError as e:
+        raise TemplateError(f"unsafe condition {cond!r}: {e}") from e
     except jinja2.UndefinedError as e:
         raise TemplateError(f"undefined variable in condition {cond!r}: {e}") from e
     except jinja2.TemplateError as e:

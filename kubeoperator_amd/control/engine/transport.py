@@ -118,8 +118,13 @@ class SSHTransport(Transport):
     name = "ssh"
 
     def __init__(self, control_dir: str | None = None, connect_timeout: int = 10, ssh_bin: str = "ssh",
-                 scp_bin: str = "scp"):
+                 scp_bin: str = "scp", known_hosts_dir: str | None = None):
         self.control_dir = control_dir or tempfile.mkdtemp(prefix="kop-ssh-")
+        os.makedirs(self.control_dir, mode=0o700, exist_ok=True)
+        # host keys are recorded on first contact (trust on first use) and checked afterwards, one
+        # known_hosts file per host:port so re-provisioned hosts can be reset individually
+        self.known_hosts_dir = known_hosts_dir or os.path.join(self.control_dir, "known_hosts")
+        os.makedirs(self.known_hosts_dir, mode=0o700, exist_ok=True)
         self.connect_timeout = connect_timeout
         self.ssh_bin, self.scp_bin = ssh_bin, scp_bin
         self._keys: dict[str, str] = {}
@@ -143,10 +148,31 @@ class SSHTransport(Transport):
                 self._keys[h] = p
             return self._keys[h]
 
+    def known_hosts_file(self, conn: HostConn) -> str:
+        safe = re.sub(r"[^A-Za-z0-9_.:-]", "_", f"{conn.address}_{conn.port}")
+        return os.path.join(self.known_hosts_dir, safe)
+
+    def forget_host_key(self, conn: HostConn) -> None:
+        """Drop a host's recorded key (after the machine was legitimately re-installed)."""
+        try:
+            os.unlink(self.known_hosts_file(conn))
+        except FileNotFoundError:
+            pass
+
+    @staticmethod
+    def _cred_tag(conn: HostConn) -> str:
+        # multiplexed masters are keyed by the credential too: after a password/key change a live master
+        # opened with the old credential is never reused
+        import hashlib
+
+        h = hashlib.sha256(f"{conn.user}\0{conn.password or ''}\0{conn.private_key or ''}".encode())
+        return h.hexdigest()[:10]
+
     def _base(self, conn: HostConn) -> tuple[list[str], dict]:
-        opts = ["-o", "StrictHostKeyChecking=no", "-o", "UserKnownHostsFile=/dev/null", "-o", "LogLevel=ERROR",
-                "-o", f"ConnectTimeout={self.connect_timeout}", "-o", "ControlMaster=auto",
-                "-o", "ControlPersist=120s", "-o", f"ControlPath={self.control_dir}/%C", "-o", "ServerAliveInterval=30"]
+        opts = ["-o", "StrictHostKeyChecking=accept-new", "-o", f"UserKnownHostsFile={self.known_hosts_file(conn)}",
+                "-o", "LogLevel=ERROR", "-o", f"ConnectTimeout={self.connect_timeout}", "-o", "ControlMaster=auto",
+                "-o", "ControlPersist=120s", "-o", f"ControlPath={self.control_dir}/{self._cred_tag(conn)}-%C",
+                "-o", "ServerAliveInterval=30"]
         env = dict(os.environ)
         kf = self._keyfile(conn)
         if kf:
@@ -210,7 +236,7 @@ class SSHTransport(Transport):
     def close(self):
         for name in os.listdir(self.control_dir) if os.path.isdir(self.control_dir) else []:
             path = os.path.join(self.control_dir, name)
-            if not name.startswith(".") and name != "askpass.sh":
+            if not name.startswith(".") and name not in ("askpass.sh", "known_hosts"):
                 subprocess.run([self.ssh_bin, "-o", f"ControlPath={path}", "-O", "exit", "dummy"],
                                capture_output=True, timeout=10)
 

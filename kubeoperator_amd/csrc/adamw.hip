@@ -8,6 +8,9 @@
 // At Llama-3-8B that is ~225 GB per step, i.e. HBM-bound at ~35 ms; with ZeRO-1 each rank runs it
 // over its 1/N shard only.
 //
+// Gradients may be bf16 (default) or fp32 (``--grad-dtype fp32``: micro-batch accumulation and the
+// data-parallel reduction in fp32, 30 B/param per step instead of 28).
+//
 // grad scaling: g_eff = g * gscale * (gscale_dev ? *gscale_dev : 1) -- gscale_dev carries a
 // device-computed clip coefficient so gradient clipping needs no host sync.
 #include "common.h"
@@ -18,7 +21,21 @@ namespace kop {
 // Every byte is touched exactly once per step. Plain (cached) loads and stores: non-temporal ones measured
 // 1 % slower on the whole training step (the update overlaps the next forward). The update uses the
 // hardware sqrt / reciprocal.
-__global__ void __launch_bounds__(256) adamw_kernel(bf16_t* __restrict__ p, const bf16_t* __restrict__ g,
+// eight consecutive gradients as fp32 (one 16-byte bf16 load or two 16-byte fp32 loads)
+__device__ __forceinline__ void load_grad8(const bf16_t* __restrict__ g, int64_t it, float* f) {
+  unpack8(reinterpret_cast<const u32x4*>(g)[it], f);
+}
+__device__ __forceinline__ void load_grad8(const float* __restrict__ g, int64_t it, float* f) {
+  const f32x4 a = reinterpret_cast<const f32x4*>(g)[it * 2], b = reinterpret_cast<const f32x4*>(g)[it * 2 + 1];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[i] = a[i];
+    f[i + 4] = b[i];
+  }
+}
+
+template <typename GT>
+__global__ void __launch_bounds__(256) adamw_kernel(bf16_t* __restrict__ p, const GT* __restrict__ g,
                                                     float* __restrict__ master, float* __restrict__ m,
                                                     float* __restrict__ v, int64_t n8, float lr, float b1, float b2,
                                                     float eps, float wd, float inv_bc1, float inv_sqrt_bc2,
@@ -30,12 +47,11 @@ __global__ void __launch_bounds__(256) adamw_kernel(bf16_t* __restrict__ p, cons
     f32x4* mp = reinterpret_cast<f32x4*>(master) + it * 2;
     f32x4* mm = reinterpret_cast<f32x4*>(m) + it * 2;
     f32x4* vv = reinterpret_cast<f32x4*>(v) + it * 2;
-    const u32x4 graw = reinterpret_cast<const u32x4*>(g)[it];
+    float gf[8], w[8], mv[8], vv8[8];
+    load_grad8(g, it, gf);
     const f32x4 w0 = mp[0], w1 = mp[1];
     const f32x4 m0 = mm[0], m1 = mm[1];
     const f32x4 v0 = vv[0], v1 = vv[1];
-    float gf[8], w[8], mv[8], vv8[8];
-    unpack8(graw, gf);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       w[i] = w0[i]; w[i + 4] = w1[i];
@@ -60,23 +76,36 @@ __global__ void __launch_bounds__(256) adamw_kernel(bf16_t* __restrict__ p, cons
   }
 }
 
-int adamw_step(bf16_t* p, const bf16_t* g, float* master, float* m, float* v, int64_t n, float lr, float b1, float b2,
-               float eps, float wd, int step, float gscale, const float* gscale_dev, hipStream_t stream) {
+template <typename GT>
+static int adamw_launch(bf16_t* p, const GT* g, float* master, float* m, float* v, int64_t n, float lr, float b1,
+                        float b2, float eps, float wd, int step, float gscale, const float* gscale_dev,
+                        hipStream_t stream) {
   if (n % 8 != 0) return -1;
   const double bc1 = 1.0 - pow((double)b1, step), bc2 = 1.0 - pow((double)b2, step);
-  adamw_kernel<<<stream_grid(n / 8, 256), 256, 0, stream>>>(p, g, master, m, v, n / 8, lr, b1, b2, eps, wd,
-                                                            (float)(1.0 / bc1), (float)(1.0 / sqrt(bc2)), gscale,
-                                                            gscale_dev);
+  adamw_kernel<GT><<<stream_grid(n / 8, 256), 256, 0, stream>>>(p, g, master, m, v, n / 8, lr, b1, b2, eps, wd,
+                                                                (float)(1.0 / bc1), (float)(1.0 / sqrt(bc2)), gscale,
+                                                                gscale_dev);
   return 0;
 }
 
-// sum of squares of a bf16 buffer, accumulated (atomically, one add per block) into out[0]
-__global__ void __launch_bounds__(256) sumsq_kernel(const bf16_t* __restrict__ g, int64_t n8, float* __restrict__ out) {
+int adamw_step(bf16_t* p, const bf16_t* g, float* master, float* m, float* v, int64_t n, float lr, float b1, float b2,
+               float eps, float wd, int step, float gscale, const float* gscale_dev, hipStream_t stream) {
+  return adamw_launch(p, g, master, m, v, n, lr, b1, b2, eps, wd, step, gscale, gscale_dev, stream);
+}
+
+int adamw_step(bf16_t* p, const float* g, float* master, float* m, float* v, int64_t n, float lr, float b1, float b2,
+               float eps, float wd, int step, float gscale, const float* gscale_dev, hipStream_t stream) {
+  return adamw_launch(p, g, master, m, v, n, lr, b1, b2, eps, wd, step, gscale, gscale_dev, stream);
+}
+
+// sum of squares of a bf16 / fp32 buffer, accumulated (atomically, one add per block) into out[0]
+template <typename GT>
+__global__ void __launch_bounds__(256) sumsq_kernel(const GT* __restrict__ g, int64_t n8, float* __restrict__ out) {
   __shared__ float red[4];
   float a = 0.f;
   for (int64_t it = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; it < n8; it += (int64_t)gridDim.x * blockDim.x) {
     float f[8];
-    unpack8(reinterpret_cast<const u32x4*>(g)[it], f);
+    load_grad8(g, it, f);
 #pragma unroll
     for (int i = 0; i < 8; ++i) a += f[i] * f[i];
   }
@@ -86,7 +115,13 @@ __global__ void __launch_bounds__(256) sumsq_kernel(const bf16_t* __restrict__ g
 
 int grad_sumsq(const bf16_t* g, int64_t n, float* out, hipStream_t stream) {
   if (n % 8 != 0) return -1;
-  sumsq_kernel<<<stream_grid(n / 8, 256), 256, 0, stream>>>(g, n / 8, out);
+  sumsq_kernel<bf16_t><<<stream_grid(n / 8, 256), 256, 0, stream>>>(g, n / 8, out);
+  return 0;
+}
+
+int grad_sumsq(const float* g, int64_t n, float* out, hipStream_t stream) {
+  if (n % 8 != 0) return -1;
+  sumsq_kernel<float><<<stream_grid(n / 8, 256), 256, 0, stream>>>(g, n / 8, out);
   return 0;
 }
 

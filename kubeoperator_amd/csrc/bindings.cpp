@@ -214,7 +214,8 @@ void adamw_(const Tensor& p, const Tensor& g, const Tensor& master, const Tensor
             double b1, double b2, double eps, double wd, int64_t step, double gscale,
             const c10::optional<Tensor>& gscale_dev) {
   check_bf16(p, "param");
-  check_bf16(g, "grad");
+  TORCH_CHECK(g.scalar_type() == at::kBFloat16 || g.scalar_type() == at::kFloat, "grad must be bf16 or fp32");
+  TORCH_CHECK(g.device() == p.device(), "grad on another device");
   check_f32(master, "master");
   check_f32(m, "exp_avg");
   check_f32(v, "exp_avg_sq");
@@ -229,16 +230,27 @@ void adamw_(const Tensor& p, const Tensor& g, const Tensor& master, const Tensor
     check_f32(*gscale_dev, "gscale_dev");
     gd = gscale_dev->data_ptr<float>();
   }
-  rc(kop::adamw_step(bp(p), bp(g), master.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), n, (float)lr,
-                     (float)b1, (float)b2, (float)eps, (float)wd, (int)step, (float)gscale, gd, cur_stream()),
-     "adamw");
+  if (g.scalar_type() == at::kFloat)
+    rc(kop::adamw_step(bp(p), g.data_ptr<float>(), master.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                       n, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (int)step, (float)gscale, gd,
+                       cur_stream()),
+       "adamw");
+  else
+    rc(kop::adamw_step(bp(p), bp(g), master.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), n,
+                       (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (int)step, (float)gscale, gd,
+                       cur_stream()),
+       "adamw");
 }
 void grad_sumsq_(const Tensor& g, const Tensor& out) {
-  check_bf16(g, "grad");
+  TORCH_CHECK(g.is_cuda() && (g.scalar_type() == at::kBFloat16 || g.scalar_type() == at::kFloat),
+              "grad must be a bf16 or fp32 GPU tensor");
   check_f32(out, "out");
   TORCH_CHECK(g.is_contiguous(), "grad must be contiguous");
   check_aligned(g, "grad");
-  rc(kop::grad_sumsq(bp(g), g.numel(), out.data_ptr<float>(), cur_stream()), "grad_sumsq");
+  if (g.scalar_type() == at::kFloat)
+    rc(kop::grad_sumsq(g.data_ptr<float>(), g.numel(), out.data_ptr<float>(), cur_stream()), "grad_sumsq");
+  else
+    rc(kop::grad_sumsq(bp(g), g.numel(), out.data_ptr<float>(), cur_stream()), "grad_sumsq");
 }
 void clip_coef_(const Tensor& sumsq, double max_norm, const Tensor& coef, const Tensor& norm) {
   rc(kop::clip_coef(sumsq.data_ptr<float>(), (float)max_norm, coef.data_ptr<float>(), norm.data_ptr<float>(),

@@ -37,7 +37,10 @@ int cross_entropy_fwd(bf16_t* logits, int64_t ld, int64_t T, int V, const int64_
 // adamw.hip
 int adamw_step(bf16_t* p, const bf16_t* g, float* master, float* m, float* v, int64_t n, float lr, float b1, float b2,
                float eps, float wd, int step, float gscale, const float* gscale_dev, hipStream_t stream);
+int adamw_step(bf16_t* p, const float* g, float* master, float* m, float* v, int64_t n, float lr, float b1, float b2,
+               float eps, float wd, int step, float gscale, const float* gscale_dev, hipStream_t stream);
 int grad_sumsq(const bf16_t* g, int64_t n, float* out, hipStream_t stream);
+int grad_sumsq(const float* g, int64_t n, float* out, hipStream_t stream);
 int clip_coef(const float* sumsq, float max_norm, float* coef, float* norm_out, hipStream_t stream);
 
 // transpose.hip

@@ -4,7 +4,8 @@ GPU tensors always take the HIP path (``ops.load()`` raises if the extension is 
 the fp32 reference path so the whole trainer can be exercised in CPU-only CI.
 
 Weight gradients follow the flat-buffer protocol of :class:`kubeoperator_amd.parallel.flat.FlatParamStore`:
-a parameter that carries ``main_grad`` (a view into the store's flat bf16 gradient buffer) gets its gradient
+a parameter that carries ``main_grad`` (a view into the store's flat bf16 -- or, with ``grad_dtype=fp32``,
+fp32 -- gradient buffer) gets its gradient
 written (or accumulated, for gradient-accumulation micro-batches) straight into that view by the backward
 kernel / GEMM (``torch.mm(..., out=main_grad)``), and the store is notified so the data-parallel layer can
 launch the bucket's collective immediately -- no AccumulateGrad pass, no extra copy.
@@ -51,7 +52,28 @@ def _gate(*ws):
             h.store.await_param(w)
 
 
+_MM_DTYPE_OUT = [True]  # aten's mixed-dtype GEMM (bf16 operands, fp32 output) available on this build
+
+
 def _mm_into(a, b, out, accumulate):
+    if out.dtype != a.dtype:
+        # fp32 gradient buffer (``--grad-dtype fp32``) fed by bf16 operands: the GEMM accumulates in fp32 and
+        # writes / adds fp32 directly; without the mixed-dtype kernel the bf16 product is added in fp32
+        if _MM_DTYPE_OUT[0]:
+            try:
+                if accumulate:
+                    torch.ops.aten.addmm.dtype_out(out, a, b, out.dtype, beta=1, alpha=1, out=out)
+                else:
+                    torch.ops.aten.mm.dtype_out(a, b, out.dtype, out=out)
+                return
+            except (RuntimeError, NotImplementedError):
+                _MM_DTYPE_OUT[0] = False
+        prod = torch.mm(a, b)
+        if accumulate:
+            out.add_(prod)
+        else:
+            out.copy_(prod)
+        return
     if accumulate:
         out.addmm_(a, b)
     else:
@@ -188,12 +210,18 @@ class _Norm(Function):
         need_w = ctx.needs_input_grad[2]
         mg_w = getattr(w, "main_grad", None) if need_w else None
         mg_b = getattr(b, "main_grad", None) if (b is not None and ctx.needs_input_grad[3]) else None
-        dw_buf = mg_w if mg_w is not None else torch.empty_like(w)
+        # fp32 gradient buffers: the kernel writes bf16 partials, added into the fp32 buffer below
+        staged = mg_w is not None and mg_w.dtype != w.dtype
+        dw_buf = mg_w if (mg_w is not None and not staged) else torch.empty_like(w)
         db_buf = None
         if ctx.layernorm:
-            db_buf = mg_b if mg_b is not None else torch.empty_like(b)
+            db_buf = mg_b if (mg_b is not None and not staged) else torch.empty_like(b)
         acc = w._kop_hooks.accumulate_for(w) if mg_w is not None else False
-        dx = lib.norm_bwd(dy, s, w, rstd, mean, dres, dw_buf, db_buf, ctx.layernorm, acc)
+        dx = lib.norm_bwd(dy, s, w, rstd, mean, dres, dw_buf, db_buf, ctx.layernorm, acc and not staged)
+        if staged:
+            for mg, buf in ((mg_w, dw_buf), (mg_b, db_buf)):
+                if mg is not None and buf is not None:
+                    mg.add_(buf) if acc else mg.copy_(buf)
         dw = None
         if need_w:
             if mg_w is not None:

@@ -1,7 +1,7 @@
 """Flat parameter / gradient storage with a communication-bucket layout.
 
 Every trainable parameter of the model becomes a view into ONE contiguous bf16 buffer (``params``) and its
-gradient a view into ONE contiguous bf16 buffer (``grads``, exposed as ``param.main_grad``). The layout is
+gradient a view into ONE contiguous bf16 (optionally fp32) buffer (``grads``, exposed as ``param.main_grad``). The layout is
 decided once, MI355X-first:
 
 * parameters are placed in the order their gradients become ready during backward (reverse forward
@@ -97,10 +97,13 @@ class GradHooks:
 
 class FlatParamStore:
     def __init__(self, module: nn.Module, specs: list[ParamSpec], device, dtype=torch.bfloat16, world: int = 1,
-                 bucket_bytes: int = 512 * 1024 * 1024):
+                 bucket_bytes: int = 512 * 1024 * 1024, grad_dtype=None):
         self.module = module
         self.world = world
         self.dtype = dtype
+        # bf16 by default (half the collective bytes); fp32 keeps micro-batch accumulation and the
+        # data-parallel reduction in fp32 (many accumulation steps x large worlds)
+        self.grad_dtype = grad_dtype or dtype
         self.device = torch.device(device)
         names = [s.name for s in specs]
         own = dict(module.named_parameters())
@@ -139,7 +142,7 @@ class FlatParamStore:
         self.numel = off
         self.decay_end = max([b.end for b in self.buckets if b.decay], default=0)
         self.params = torch.zeros(self.numel, dtype=dtype, device=self.device)
-        self.grads = torch.zeros(self.numel, dtype=dtype, device=self.device)
+        self.grads = torch.zeros(self.numel, dtype=self.grad_dtype, device=self.device)
         self.hooks = GradHooks(self)
         self.specs = {s.name: s for s in specs}
         self.offsets = offsets
@@ -290,4 +293,4 @@ class FlatParamStore:
         return out
 
     def memory_bytes(self) -> int:
-        return self.params.numel() * self.params.element_size() * 2
+        return self.params.numel() * self.params.element_size() + self.grads.numel() * self.grads.element_size()

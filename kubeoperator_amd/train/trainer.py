@@ -38,6 +38,7 @@ class TrainConfig:
     overlap_optimizer: bool = True  # AdamW on its own stream, gated per bucket into the next forward
     transposed_weights: bool = True  # keep W^T copies of wide weights for the dX GEMMs (GPU only)
     cuda_graph: bool = False  # replay each micro-batch's forward + backward as a captured HIP graph (1 GPU)
+    grad_dtype: str = "bf16"  # bf16 | fp32: gradient buffer (micro-batch accumulation + DP reduction) precision
     seed: int = 1234
     model_overrides: dict = field(default_factory=dict)
 
@@ -63,8 +64,11 @@ class Trainer:
         t0 = time.time()
         with torch.device("meta"):
             self.model = build_model(self.cfg)
+        if tc.grad_dtype not in ("bf16", "fp32"):
+            raise ValueError(f"grad_dtype must be bf16 or fp32, not {tc.grad_dtype!r}")
         self.store = FlatParamStore(self.model, self.model.param_specs(), dev, world=info.world,
-                                    bucket_bytes=tc.bucket_mb * 1024 * 1024)
+                                    bucket_bytes=tc.bucket_mb * 1024 * 1024,
+                                    grad_dtype=torch.float32 if tc.grad_dtype == "fp32" else torch.bfloat16)
         self.store.init_weights(seed=tc.seed)
         self.dp = DataParallel(self.store, info, tc.dp_mode)
         self.dp.broadcast_params()

@@ -196,6 +196,51 @@ def test_roles_defaults_templates_and_include(tmp_path):
     assert "echo extra 8080" in t.commands("w1")
 
 
+def test_role_default_referencing_other_vars_is_expanded(tmp_path):
+    """A role default whose value is a template (Ansible's lazy var templating) must be rendered wherever it
+    is used: in a template file, a shell command, a hostvars lookup and a dict-valued var."""
+    role = tmp_path / "roles" / "rt"
+    for d in ("tasks", "defaults", "templates"):
+        (role / d).mkdir(parents=True)
+    (role / "defaults" / "main.yml").write_text(textwrap.dedent("""
+        root: "{{ STORAGE_DIR | default('/var/lib/c') }}"
+        state: "{{ root }}/state"
+        max_pods: "{{ MAX_PODS | default(110) }}"
+        opts: {dir: "{{ state }}", pods: "{{ max_pods }}"}
+    """))
+    (role / "templates" / "c.toml.j2").write_text("root = \"{{ root }}\"\nstate = \"{{ state }}\"\n"
+                                                  "pods = {{ max_pods | int + 1 }}\ndir = {{ opts.dir }}\n")
+    (role / "tasks" / "main.yml").write_text(textwrap.dedent("""
+        - template: src=c.toml.j2 dest=/etc/c.toml
+        - shell: "mkdir -p {{ root }} && echo {{ hostvars[inventory_hostname]['hv'] }}"
+    """))
+    inv = _inv()
+    inv.groups["all"].vars["hv"] = "{{ z }}-{{ STORAGE_DIR }}"
+    res, t, _ = _play(tmp_path, """
+    - hosts: gpu_nodes
+      gather_facts: false
+      roles: [rt]
+    """, inv=inv, roles_path=[str(tmp_path / "roles")], extra_vars={"STORAGE_DIR": "/data/ctr", "MAX_PODS": 200})
+    assert res["summary"]["success"], res["summary"]
+    assert t.fs["w1"]["/etc/c.toml"] == b'root = "/data/ctr"\nstate = "/data/ctr/state"\npods = 201\n' \
+                                        b'dir = /data/ctr/state\n'
+    assert "mkdir -p /data/ctr && echo all-/data/ctr" in t.commands("w1")
+
+
+def test_templates_are_sandboxed_and_recursion_bounded():
+    from kubeoperator_amd.control.engine.templating import TemplateError, render_text
+
+    evil = "{{ cycler.__init__.__globals__.os.popen('echo pwned').read() }}"
+    v = {"CLUSTER_CIDR": evil, "a": "{{ b }}", "b": "{{ a }}"}
+    for text in (evil, "{{ CLUSTER_CIDR }}", "x {{ ''.__class__.__mro__[1].__subclasses__() }}"):
+        with pytest.raises(TemplateError):
+            render(text, v)
+    with pytest.raises(TemplateError):
+        render_text("cidr={{ CLUSTER_CIDR }}\n", v)
+    with pytest.raises(TemplateError, match="recursive"):
+        render("{{ a }}", v)
+
+
 def test_adhoc():
     t = FakeTransport()
     t.add_rule(r"uptime", stdout="up 1 day")

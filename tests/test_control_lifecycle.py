@@ -3,6 +3,7 @@ from a plan template, install -> gpu-validate -> add-worker -> upgrade -> backup
 remove-worker -> uninstall, plus failure / resume / busy-lock paths. Mirrors the reference's deploy
 state machine (kubeops_api/models/deploy.py:55-230) and its per-step status tracking."""
 import os
+import re
 
 import pytest
 
@@ -59,6 +60,15 @@ def test_full_lifecycle(control):
     assert any("amdgpu" in c for c in farm.commands("w1"))
     assert not any("amdgpu-dkms" in c for c in farm.commands("m1"))
     assert "apiVersion" in clusters.fetch_kubeconfig("demo")
+    # every templated file and command is fully expanded (role defaults that reference other vars included)
+    for h, files in farm.fs.items():
+        for path, data in files.items():
+            if "/charts/" in path:  # Helm chart sources are copied verbatim (Helm renders them)
+                continue
+            assert b"{{" not in data and b"{%" not in data, (h, path)
+    assert not [c for _, c in farm.log if "{{" in c and "/charts/" not in c]
+    cfg = farm.fs["w1"]["/etc/containerd/config.toml"].decode()
+    assert re.search(r'^root = "/[^"{]+"$', cfg, re.M) and 'sandbox_image = "' in cfg
 
     assert deploy.create("demo", "gpu-validate", run="inline")["state"] == "SUCCESS"
 

@@ -131,3 +131,34 @@ def test_unarchive_and_setup_facts(tmp_path):
     """, extra={"tgz": str(tmp_path / "tool.tgz")})
     assert res["summary"]["success"], res["summary"]["dark"]
     assert (tmp_path / "out" / "opt" / "bin" / "tool").exists()
+
+
+def test_ssh_transport_pins_host_keys_and_keys_masters_by_credential(tmp_path):
+    """SSH options: trust-on-first-use host keys in a per-host known_hosts file (not disabled checking), and
+    a ControlPath that changes with the credential so a master opened with an old password is not reused."""
+    import json
+    import stat as st
+
+    from kubeoperator_amd.control.engine.transport import HostConn, SSHTransport
+
+    rec = tmp_path / "argv.jsonl"
+    fake_ssh = tmp_path / "ssh"
+    fake_ssh.write_text("#!/usr/bin/env python3\nimport json, sys\n"
+                        f"open({str(rec)!r}, 'a').write(json.dumps(sys.argv[1:]) + '\\n')\n")
+    fake_ssh.chmod(fake_ssh.stat().st_mode | st.S_IEXEC)
+    t = SSHTransport(control_dir=str(tmp_path / "ctl"), ssh_bin=str(fake_ssh),
+                     known_hosts_dir=str(tmp_path / "kh"))
+    a = HostConn("n1", "10.1.2.3", 2222, "root", password="old")
+    t.run(a, "true")
+    t.run(HostConn("n1", "10.1.2.3", 2222, "root", password="new"), "true")
+    argvs = [json.loads(line) for line in rec.read_text().splitlines()]
+
+    def opt(argv, key):
+        return [argv[i + 1].split("=", 1)[1] for i, x in enumerate(argv) if x == "-o" and
+                argv[i + 1].startswith(key + "=")][0]
+
+    assert opt(argvs[0], "StrictHostKeyChecking") == "accept-new"
+    assert opt(argvs[0], "UserKnownHostsFile") == str(tmp_path / "kh" / "10.1.2.3_2222")
+    assert opt(argvs[0], "ControlPath") != opt(argvs[1], "ControlPath")
+    assert "/dev/null" not in " ".join(argvs[0])
+    t.forget_host_key(a)  # no file yet: a no-op

@@ -126,3 +126,40 @@ def test_hip_graph_replay_matches_eager(model, accum):
     assert torch.allclose(l_e, l_g, rtol=1e-3, atol=1e-3), (l_e, l_g)
     d = (eager.store.params.float() - graphed.store.params.float()).abs().max().item()
     assert d <= 2e-3, d
+
+
+@pytest.mark.parametrize("model", ["tiny_llama", "tiny_gpt2"])
+def test_fp32_gradient_buffer_matches_bf16_path(model):
+    """``grad_dtype="fp32"``: every gradient sink (hipBLASLt GEMMs writing/accumulating fp32 through the
+    mixed-dtype GEMM, staged norm/bias gradients, embedding) and the fp32-gradient AdamW / sum-of-squares
+    kernels. Gradients after 3 accumulated micro-batches must match the bf16 buffer's to bf16 rounding, and
+    an fp32 optimizer step must track the bf16 one."""
+    from kubeoperator_amd.parallel.dist import DistInfo
+    from kubeoperator_amd.train import SyntheticTokens, TrainConfig, Trainer
+
+    def run(gd):
+        info = DistInfo(0, 0, 1, "none", torch.device("cuda", 0))
+        tc = TrainConfig(model=model, micro_batch=2, seq_len=256, grad_accum=3, warmup_steps=1, total_steps=10,
+                         bucket_mb=1, grad_dtype=gd, transposed_weights=False)
+        tr = Trainer(tc, info)
+        data = SyntheticTokens(tr.cfg.vocab_size, 2, 256, info.device, seed=11)
+        batches = list(data.batches(3))
+        for i, (x, y) in enumerate(batches):  # gradients only
+            tr.store.begin_microbatch(i)
+            tr.model(x, y).backward()
+        torch.cuda.synchronize()
+        grads = tr.store.grads.float().clone()
+        loss = tr.train_step(iter(batches))
+        tr.store.await_all()
+        torch.cuda.synchronize()
+        return tr, grads, float(loss)
+
+    b16, g16, l16 = run("bf16")
+    f32, g32, l32 = run("fp32")
+    assert f32.store.grads.dtype == torch.float32
+    rel = ((g32 - g16).norm() / g16.norm()).item()
+    assert rel < 1e-2, rel
+    assert abs(l16 - l32) < 1e-3
+    assert torch.isfinite(f32.store.params.float()).all()
+    prel = ((f32.store.params.float() - b16.store.params.float()).norm() / b16.store.params.float().norm()).item()
+    assert prel < 1e-2, prel

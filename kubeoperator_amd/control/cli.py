@@ -6,6 +6,10 @@ with pidfiles, and the host-side ``kubeopsctl.sh``):
     kubeopsctl init                          # create the store, seed admin / item / settings
     kubeopsctl start [all|web|worker|beat] [-d]
     kubeopsctl stop|status|restart [all|web|worker|beat]
+    kubeopsctl install [--start] | uninstall [--purge] | upgrade     # the operator itself (5/6/7_*.sh)
+    kubeopsctl reload [SVC] | down [SVC] | tail [SVC] [-n N] [-f]    # (re)start, stop + clean, follow logs
+    kubeopsctl python [-c CODE] | db [-c SQL]                         # shell with the store loaded / SQL shell
+    kubeopsctl exec SVC [-- CMD]                                      # a shell in the service's environment
 
 Cluster operations (the UI's flows, usable headless; ``--server URL`` talks to a running control plane over
 the REST API, otherwise the store is used in-process and operations run inline with their log on stdout):
@@ -170,6 +174,220 @@ def cmd_status(a, cfg) -> int:
         print(f"{s}: {'running (pid %d)' % pid if pid else 'stopped'}")
         rc |= 0 if pid else 3
     return rc
+
+
+# ------------------------------------------------------------------------- operator lifecycle (kubeopsctl.sh)
+_UNIT = """[Unit]
+Description=KubeOperator-AMD control plane (API, workers, scheduler)
+After=network-online.target
+
+[Service]
+Type=simple
+Environment=KUBEOPERATOR_CONFIG={config}
+ExecStart={python} -m kubeoperator_amd.control.cli start all
+ExecReload={python} -m kubeoperator_amd.control.cli reload
+Restart=on-failure
+WorkingDirectory={data}
+
+[Install]
+WantedBy=multi-user.target
+"""
+
+
+def _unit_path(cfg) -> str:
+    return os.path.join(cfg.data_dir, "kubeops.service")
+
+
+def _config_path(a, cfg) -> str:
+    return a.config or os.environ.get("KUBEOPERATOR_CONFIG") or os.path.join(cfg.data_dir, "config.yml")
+
+
+def cmd_install(a, cfg) -> int:
+    """Reference scripts/5_install.sh: prepare the data directory, store, default config and service unit
+    (systemd runs ``kubeopsctl start all``; ``scripts/install.sh`` adds the environment checks and the compose
+    mode). ``--start`` starts the services in the background right away."""
+    os.makedirs(cfg.data_dir, exist_ok=True)
+    conf = _config_path(a, cfg)
+    if not os.path.exists(conf):
+        with open(conf, "w") as f:
+            yaml.safe_dump({"DATA_DIR": cfg.data_dir, "HTTP_LISTEN_PORT": int(cfg["HTTP_LISTEN_PORT"]),
+                            "DEFAULT_TRANSPORT": cfg["DEFAULT_TRANSPORT"]}, f)
+        os.chmod(conf, 0o600)
+    with open(_unit_path(cfg), "w") as f:
+        f.write(_UNIT.format(config=conf, python=sys.executable, data=cfg.data_dir))
+    print(f"data dir:  {cfg.data_dir}\nconfig:    {conf}\nstore:     {cfg.db_url}\n"
+          f"unit file: {_unit_path(cfg)}  (install with: cp {_unit_path(cfg)} /etc/systemd/system/ && "
+          f"systemctl enable --now kubeops)")
+    if a.start:
+        a.service, a.daemon = "all", True
+        return cmd_start(a, cfg)
+    return 0
+
+
+def cmd_uninstall(a, cfg) -> int:
+    """Reference scripts/6_uninstall.sh: stop every service, remove the unit; ``--purge`` also deletes the data
+    directory (store, logs, execution logs, backups kept locally)."""
+    a.service = "all"
+    cmd_stop(a, cfg)
+    try:
+        os.remove(_unit_path(cfg))
+    except OSError:
+        pass
+    if a.purge:
+        import shutil
+
+        from .store import db
+        db.engine().dispose()
+        d = cfg.data_dir  # (the property creates the directory on access)
+        shutil.rmtree(d, ignore_errors=True)
+        print(f"removed {d}")
+    return 0
+
+
+def cmd_upgrade(a, cfg) -> int:
+    """Reference scripts/7_upgrade.sh: stop, back up the store, migrate the schema, restart what was running."""
+    from .store import db
+
+    was = [s for s in SERVICES if _read_pid(cfg, s)]
+    if was:
+        a.service = "all"
+        cmd_stop(a, cfg)
+    url = cfg.db_url
+    if url.startswith("sqlite:///"):
+        import sqlite3
+
+        path = url[len("sqlite:///"):]
+        if os.path.exists(path):
+            bak = f"{path}.{time.strftime('%Y%m%d%H%M%S')}.bak"
+            src, dst = sqlite3.connect(path), sqlite3.connect(bak)
+            with dst:
+                src.backup(dst)
+            src.close()
+            dst.close()
+            print(f"store backed up to {bak}")
+    db.init_db()
+    print(f"schema at version {db.SCHEMA_VERSION}")
+    if was:
+        a.service, a.daemon = "all", True
+        return cmd_start(a, cfg)
+    return 0
+
+
+def cmd_reload(a, cfg) -> int:
+    """Restart (or start) the given services in the background (reference ``reload``: up -d + restart)."""
+    cmd_stop(a, cfg)
+    a.daemon = True
+    return cmd_start(a, cfg)
+
+
+def cmd_down(a, cfg) -> int:
+    """Stop the services and clear their runtime state (pidfiles, SSH control sockets)."""
+    cmd_stop(a, cfg)
+    for name in os.listdir(_pid_dir(cfg)):
+        if name.endswith(".pid") and (a.service in ("all", None) or name == f"{a.service}.pid"):
+            os.remove(os.path.join(_pid_dir(cfg), name))
+    return 0
+
+
+def _log_files(cfg, svc) -> list[str]:
+    files = [os.path.join(_pid_dir(cfg), "kubeops.log")]
+    logdir = os.path.join(cfg.data_dir, "logs")
+    if os.path.isdir(logdir):
+        files += sorted(os.path.join(logdir, f) for f in os.listdir(logdir) if f.endswith(".jsonl"))[-1:]
+    return [f for f in files if os.path.exists(f)]
+
+
+def cmd_tail(a, cfg, out=None) -> int:
+    """Last N lines of the service log (``-f`` follows it). With a service name, only its lines."""
+    out = out or sys.stdout
+    files = _log_files(cfg, a.service)
+    if not files:
+        print("no logs yet", file=out)
+        return 1
+    path = files[0]
+    want = None if a.service in ("all", None) else a.service
+
+    def keep(line):
+        return want is None or want in line or (want == "web" and "api" in line) or \
+            (want == "worker" and "jobs" in line) or (want == "beat" and "scheduler" in line)
+
+    with open(path, errors="replace") as f:
+        lines = [ln for ln in f.readlines() if keep(ln)]
+        for ln in lines[-a.lines:]:
+            out.write(ln)
+        out.flush()
+        while a.follow:
+            ln = f.readline()
+            if not ln:
+                time.sleep(0.3)
+                continue
+            if keep(ln):
+                out.write(ln)
+                out.flush()
+    return 0
+
+
+def cmd_python(a, cfg) -> int:
+    """Interactive Python with the store configured (reference ``python manage.py shell``)."""
+    from .domain import clusters, deploy, hosts  # noqa: F401
+    from .store import models as M  # noqa: F401
+    from .store.db import session_scope  # noqa: F401
+    ns = {k: v for k, v in locals().items() if k not in ("a",)}
+    if a.code:
+        exec(compile(a.code, "<kubeopsctl python -c>", "exec"), ns)
+        return 0
+    import code
+
+    code.interact(banner="KubeOperator-AMD shell: clusters, deploy, hosts, M (models), session_scope", local=ns)
+    return 0
+
+
+def cmd_db(a, cfg, out=None) -> int:
+    """SQL against the store (reference ``manage.py dbshell``): ``-c SQL`` runs one statement, otherwise a
+    read-eval-print loop (``.tables`` lists the tables)."""
+    from sqlalchemy import inspect, text
+
+    from .store import db
+    out = out or sys.stdout
+
+    def run(sql):
+        sql = sql.strip().rstrip(";")
+        if not sql:
+            return
+        if sql == ".tables":
+            print("  ".join(sorted(inspect(db.engine()).get_table_names())), file=out)
+            return
+        with db.engine().begin() as c:
+            res = c.execute(text(sql))
+            if res.returns_rows:
+                cols = list(res.keys())
+                print("|".join(cols), file=out)
+                for row in res:
+                    print("|".join("" if v is None else str(v) for v in row), file=out)
+            else:
+                print(f"{res.rowcount} row(s)", file=out)
+
+    if a.code:
+        run(a.code)
+        return 0
+    while True:
+        try:
+            line = input("kubeops-db> ")
+        except EOFError:
+            return 0
+        if line.strip() in (".quit", ".exit", "\\q"):
+            return 0
+        try:
+            run(line)
+        except Exception as e:  # noqa: BLE001 -- a REPL reports and continues
+            print(f"error: {e}", file=out)
+
+
+def cmd_exec_service(a, cfg) -> int:
+    """A shell (or ``CMD``) in the environment the services run with (reference ``exec`` into a container)."""
+    env = dict(os.environ, KUBEOPERATOR_CONFIG=_config_path(a, cfg), KUBEOPERATOR_SERVICE=a.action)
+    argv = a.rest[1:] if a.rest and a.rest[0] == "--" else (a.rest or [os.environ.get("SHELL", "/bin/bash")])
+    return subprocess.call(argv, env=env, cwd=cfg.data_dir)
 
 
 # ------------------------------------------------------------------------------------------------ backends
@@ -451,11 +669,19 @@ def main(argv=None) -> int:
     sub = ap.add_subparsers(dest="cmd", required=True)
     sub.add_parser("init")
     sub.add_parser("version")
-    for name in ("start", "stop", "status", "restart"):
+    for name in ("start", "stop", "status", "restart", "reload", "down", "tail"):
         p = sub.add_parser(name)
         p.add_argument("service", nargs="?", default="all", choices=["all", *SERVICES])
         if name in ("start", "restart"):
             p.add_argument("-d", "--daemon", action="store_true")
+        if name == "tail":
+            p.add_argument("-n", "--lines", type=int, default=100)
+            p.add_argument("-f", "--follow", action="store_true")
+    sub.add_parser("install").add_argument("--start", action="store_true")
+    sub.add_parser("uninstall").add_argument("--purge", action="store_true")
+    sub.add_parser("upgrade")
+    sub.add_parser("python").add_argument("-c", dest="code")
+    sub.add_parser("db").add_argument("-c", dest="code")
     c = sub.add_parser("cluster")
     c.add_argument("action", choices=["create", "list", "show", "kubeconfig", "delete", "install", "uninstall",
                                       "scale", "add-worker", "remove-worker", "upgrade", "backup", "restore",
@@ -480,8 +706,9 @@ def main(argv=None) -> int:
     h.add_argument("--credential")
     h.add_argument("--file")
     e = sub.add_parser("exec")
-    e.add_argument("action", choices=["list", "log"])
-    e.add_argument("target")
+    e.add_argument("action", choices=["list", "log", *SERVICES])
+    e.add_argument("target", nargs="?")
+    e.add_argument("rest", nargs=argparse.REMAINDER)
     sub.add_parser("package").add_argument("action", nargs="?", default="list", choices=["list"])
     a = ap.parse_args(argv)
 
@@ -502,6 +729,14 @@ def main(argv=None) -> int:
     if a.cmd == "restart":
         cmd_stop(a, cfg)
         return cmd_start(a, cfg)
+    simple = {"install": cmd_install, "uninstall": cmd_uninstall, "upgrade": cmd_upgrade, "reload": cmd_reload,
+              "down": cmd_down, "tail": cmd_tail, "python": cmd_python, "db": cmd_db}
+    if a.cmd in simple:
+        return simple[a.cmd](a, cfg)
+    if a.cmd == "exec" and a.action in SERVICES:
+        if a.target:
+            a.rest = [a.target, *a.rest]
+        return cmd_exec_service(a, cfg)
     if a.cmd == "host" and a.action == "import":
         a.file = a.file or a.name
     return {"cluster": cmd_cluster, "host": cmd_host, "exec": cmd_exec, "package": cmd_package}[a.cmd](a, cfg)

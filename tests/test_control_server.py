@@ -120,3 +120,40 @@ def test_service_launcher(tmp_path):
             break
         time.sleep(0.1)
     assert "stopped" in run("status", "worker").stdout
+
+
+def test_operator_lifecycle_verbs(tmp_path):
+    """kubeopsctl install / db / python / upgrade / reload / tail / down / uninstall --purge (reference
+    kubeopsctl.sh verbs, re-done for a process-based deployment)."""
+    cfgp = tmp_path / "config.yml"
+    data = tmp_path / "data"
+    cfgp.write_text(f"DATA_DIR: {data}\nHTTP_LISTEN_PORT: 0\nHTTP_BIND_HOST: 127.0.0.1\n")
+    env = dict(os.environ, KUBEOPERATOR_CONFIG=str(cfgp), KOP_PBKDF2_ITERS="1000")
+    run = lambda *a: subprocess.run([sys.executable, "-m", "kubeoperator_amd.control.cli", *a], env=env,  # noqa: E731
+                                    capture_output=True, text=True, timeout=60)
+    r = run("install")
+    assert r.returncode == 0, r.stderr
+    unit = (data / "kubeops.service").read_text()
+    assert "ExecStart=" in unit and "start all" in unit and str(cfgp) in unit
+    r = run("db", "-c", "select username from users")
+    assert r.returncode == 0 and "admin" in r.stdout, r.stdout + r.stderr
+    r = run("python", "-c", "from sqlalchemy import select\nwith session_scope() as s: print(len(s.scalars(select(M.User)).all()))")
+    assert r.returncode == 0 and r.stdout.strip() == "1", r.stdout + r.stderr
+    r = run("upgrade")
+    assert r.returncode == 0 and "backed up" in r.stdout, r.stdout + r.stderr
+    r = run("reload", "worker")
+    assert r.returncode == 0, r.stdout + r.stderr
+    try:
+        assert "running" in run("status", "worker").stdout
+        time.sleep(0.5)
+        r = run("tail", "-n", "5")
+        assert r.returncode in (0, 1)
+    finally:
+        r = run("down", "worker")
+    for _ in range(50):
+        if "stopped" in run("status", "worker").stdout:
+            break
+        time.sleep(0.1)
+    assert not list((data / "tmp").glob("*.pid"))
+    r = run("uninstall", "--purge")
+    assert r.returncode == 0 and not data.exists()

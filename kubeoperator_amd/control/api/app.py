@@ -509,6 +509,33 @@ def create_app() -> FastAPI:
         _cluster_for(current_user(request), name)
         return deploy.get(eid)
 
+    @r.get("/clusters/{name}/apps/")
+    def list_cluster_apps(name: str, request: Request):
+        """Helm releases deployed through ``app-deploy`` executions (training runs carry their result)."""
+        c = _cluster_for(current_user(request), name)
+        return clusters.list_apps(c.name)
+
+    @r.get("/apps/catalog/")
+    def app_catalog(request: Request):
+        """Bundled charts and their default values (the app store content shipped with the operator)."""
+        current_user(request)
+        import yaml as _yaml
+
+        from ..domain import plan as _plan
+        root = os.path.join(_plan.PLAYBOOK_DIR, "roles", "kubeapps", "files", "charts")
+        out = []
+        for d in sorted(os.listdir(root)):
+            try:
+                with open(os.path.join(root, d, "Chart.yaml")) as f:
+                    meta = _yaml.safe_load(f)
+                with open(os.path.join(root, d, "values.yaml")) as f:
+                    values = _yaml.safe_load(f) or {}
+            except OSError:
+                continue
+            out.append({"name": meta.get("name", d), "version": meta.get("version"),
+                        "description": meta.get("description", ""), "values": values})
+        return out
+
     @r.get("/cluster/config")
     @r.get("/cluster/config/")
     def cluster_plan(request: Request):

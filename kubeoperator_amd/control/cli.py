@@ -23,6 +23,9 @@ the REST API, otherwise the store is used in-process and operations run inline w
     kubeopsctl cluster backup NAME --storage S | restore NAME --backup ID
     kubeopsctl cluster gpu-validate NAME | list | show NAME | kubeconfig NAME | delete NAME
     kubeopsctl exec list NAME | exec log ID
+    kubeopsctl app deploy NAME --chart nginx|pytorch-rocm-train [--release R] [--namespace N] [--set k=v ...]
+                   [--wait-job]                  # Helm release; a training run reports its tokens/s
+    kubeopsctl app list NAME | app remove NAME --release R [--namespace N]
     kubeopsctl package list
 """
 from __future__ import annotations
@@ -425,6 +428,9 @@ class Local:
             self.clusters.add_node(plan_doc["name"], n)
         return self.clusters.cluster_dict(self.clusters.get_cluster(out["id"]))
 
+    def list_apps(self, name):
+        return self.clusters.list_apps(name)
+
     def operate(self, name, op, params):
         from .runtime import jobs
 
@@ -521,6 +527,9 @@ class Remote:
         for h in plan_doc.get("hosts") or []:
             self.http.post("/host/", json=h)
         return self._j(self.http.post("/clusters/", json=plan_doc))
+
+    def list_apps(self, name):
+        return self._j(self.http.get(f"/clusters/{name}/apps/"))
 
     def operate(self, name, op, params):
         e = self._j(self.http.post(f"/clusters/{name}/executions/", json={"operation": op, "params": params}))
@@ -625,6 +634,39 @@ def cmd_cluster(a, cfg) -> int:
     return _finish(b.operate(a.name, op, params))
 
 
+def _set_values(pairs) -> dict:
+    """``--set a.b=1`` (helm style, dotted keys, YAML-typed values) -> nested dict."""
+    out: dict = {}
+    for kv in pairs or []:
+        k, _, v = kv.partition("=")
+        cur = out
+        parts = k.split(".")
+        for p in parts[:-1]:
+            cur = cur.setdefault(p, {})
+        cur[parts[-1]] = yaml.safe_load(v) if v != "" else ""
+    return out
+
+
+def cmd_app(a, cfg) -> int:
+    b = _backend(a)
+    if a.action == "list":
+        rows = [dict(r, result=(f"{r['training']['tokens_per_s']:.0f} tok/s" if r.get("training") else ""))
+                for r in b.list_apps(a.name)]
+        _table(rows, ["namespace", "release", "chart", "date", "result"])
+        return 0
+    params = {"chart": a.chart, "namespace": a.namespace}
+    if a.release:
+        params["release"] = a.release
+    if a.action == "deploy":
+        params.update(values=_set_values(a.set), wait_job=a.wait_job)
+        res = b.operate(a.name, "app-deploy", params)
+        run = (res.get("result_summary") or {}).get("training")
+        if run:
+            print(json.dumps({"training": run}))
+        return _finish(res)
+    return _finish(b.operate(a.name, "app-remove", params))
+
+
 def cmd_host(a, cfg) -> int:
     b = _backend(a)
     if a.action == "add":
@@ -710,6 +752,14 @@ def main(argv=None) -> int:
     e.add_argument("target", nargs="?")
     e.add_argument("rest", nargs=argparse.REMAINDER)
     sub.add_parser("package").add_argument("action", nargs="?", default="list", choices=["list"])
+    ap_ = sub.add_parser("app")
+    ap_.add_argument("action", choices=["deploy", "list", "remove"])
+    ap_.add_argument("name", help="cluster")
+    ap_.add_argument("--chart", default="nginx")
+    ap_.add_argument("--release")
+    ap_.add_argument("--namespace", default="default")
+    ap_.add_argument("--set", action="append", help="value override k=v (dotted keys)")
+    ap_.add_argument("--wait-job", action="store_true", help="wait for the release's Job and collect its result")
     a = ap.parse_args(argv)
 
     if a.cmd == "version":
@@ -739,7 +789,8 @@ def main(argv=None) -> int:
         return cmd_exec_service(a, cfg)
     if a.cmd == "host" and a.action == "import":
         a.file = a.file or a.name
-    return {"cluster": cmd_cluster, "host": cmd_host, "exec": cmd_exec, "package": cmd_package}[a.cmd](a, cfg)
+    return {"cluster": cmd_cluster, "host": cmd_host, "exec": cmd_exec, "package": cmd_package,
+            "app": cmd_app}[a.cmd](a, cfg)
 
 
 if __name__ == "__main__":

@@ -179,6 +179,24 @@ def set_config(cluster_name: str, key: str, value) -> None:
         c.configs = {**(c.configs or {}), key: value}
 
 
+def record_app(cluster_name: str, op: str, rel: dict) -> None:
+    """Keep the cluster's Helm releases (``configs["app_releases"]``, keyed by namespace/release)."""
+    key = f"{rel['namespace']}/{rel['release']}"
+    with session_scope() as s:
+        c = s.scalar(select(M.Cluster).where(M.Cluster.name == cluster_name).with_for_update())
+        apps = dict((c.configs or {}).get("app_releases") or {})
+        if op == "app-remove":
+            apps.pop(key, None)
+        else:
+            apps[key] = dict(rel, date=M.now().isoformat())
+        c.configs = {**(c.configs or {}), "app_releases": apps}
+
+
+def list_apps(cluster_name: str) -> list[dict]:
+    return sorted((get_cluster(cluster_name).configs or {}).get("app_releases", {}).values(),
+                  key=lambda a: (a["namespace"], a["release"]))
+
+
 def del_config(cluster_name: str, key: str) -> None:
     # (the reference edits a non-existent ``self.vars`` here, cluster.py:296-300)
     with session_scope() as s:

@@ -3,7 +3,10 @@
 Operations (same names and params as the reference API): ``install``, ``uninstall``, ``bigip-config``,
 ``upgrade`` {package}, ``scale`` {num}, ``add-worker`` {host}, ``remove-worker`` {node},
 ``backup`` {backupStorageId}, ``restore`` {clusterBackupId}, plus ``gpu-validate`` (run the rocminfo
-validation pod on every GPU worker).
+validation pod on every GPU worker), ``app-deploy`` {chart, release, namespace, values, wait_job} and
+``app-remove`` {release, namespace}: Helm releases of the bundled charts (nginx, the PyTorch-ROCm training
+chart) recorded on the cluster; a training release run with ``wait_job`` gets its last logged step
+(tokens/s, step time, loss) attached to the execution result.
 
 Per operation: cluster status while running -> after (INSTALLING -> RUNNING/ERROR, DELETING -> READY,
 UPGRADING, SCALING, BACKUP, RESTORING -> RUNNING); ``ignore_errors`` operations (scale / add / remove /
@@ -17,7 +20,9 @@ idempotent), and ``timedelta`` is recorded in float seconds -- the cluster-creat
 """
 from __future__ import annotations
 
+import json
 import logging
+import re
 import time
 
 from sqlalchemy import select
@@ -30,7 +35,9 @@ from . import clusters, context, plan
 log = logging.getLogger("kubeoperator.deploy")
 
 OPERATIONS = ("install", "uninstall", "bigip-config", "upgrade", "scale", "add-worker", "remove-worker", "backup",
-              "restore", "gpu-validate")
+              "restore", "gpu-validate", "app-deploy", "app-remove")
+_DNS1123 = re.compile(r"^[a-z0-9]([-a-z0-9]{0,51}[a-z0-9])?$")
+_CHART = re.compile(r"^[A-Za-z0-9][A-Za-z0-9._-]*(/[A-Za-z0-9][A-Za-z0-9._-]*)?$")
 IGNORE_ERRORS = {"bigip-config", "scale", "add-worker", "remove-worker"}
 RETURN_RUNNING = {"scale", "add-worker", "remove-worker"}
 RUNNING_STATUS = {"install": "INSTALLING", "uninstall": "DELETING", "upgrade": "UPGRADING", "scale": "SCALING",
@@ -38,7 +45,8 @@ RUNNING_STATUS = {"install": "INSTALLING", "uninstall": "DELETING", "upgrade": "
 OPERATION_NAME = {"install": "Cluster install", "uninstall": "Cluster uninstall", "upgrade": "Cluster upgrade",
                   "scale": "Cluster scale", "add-worker": "Cluster scale", "remove-worker": "Cluster scale",
                   "restore": "Cluster restore", "backup": "Cluster backup", "bigip-config": "F5 BIG-IP config",
-                  "gpu-validate": "GPU validation"}
+                  "gpu-validate": "GPU validation", "app-deploy": "Application deploy",
+                  "app-remove": "Application remove"}
 
 
 def create(cluster_name: str, operation: str, params: dict | None = None, user: str = "",
@@ -48,6 +56,8 @@ def create(cluster_name: str, operation: str, params: dict | None = None, user: 
         raise ValueError(f"unknown operation {operation!r}; one of {OPERATIONS}")
     c = clusters.get_cluster(cluster_name)
     params = dict(params or {})
+    if operation in ("app-deploy", "app-remove"):
+        _check_app_params(operation, params)
     with session_scope() as s:
         busy = s.scalar(select(M.Execution).where(M.Execution.project_id == c.project_id, M.Execution.kind == "deploy",
                                                   M.Execution.state.in_(("PENDING", "STARTED"))))
@@ -288,7 +298,58 @@ def _dispatch(ex: _Exec, c: M.Cluster, ev: dict) -> dict:
     if op == "gpu-validate":
         ex.set_steps("gpu-validate")
         return ex.run_playbooks(ev)
+    if op in ("app-deploy", "app-remove"):
+        p = ex.params
+        chart = p.get("chart", "nginx")
+        ev.update(app_chart=chart, app_release=p.get("release") or chart.split("/")[-1],
+                  app_namespace=p.get("namespace", "default"), app_values=p.get("values") or {},
+                  app_wait_job=bool(p.get("wait_job", False)))
+        if p.get("timeout"):
+            ev["app_timeout"] = str(p["timeout"])
+        ex.set_steps(op)
+        res = ex.run_playbooks(ev)
+        if res["summary"].get("success"):
+            run = _training_result(res.get("raw") or {}) if op == "app-deploy" else None
+            if run:
+                res["summary"]["training"] = run
+            clusters.record_app(c.name, op, {"release": ev["app_release"], "chart": chart,
+                                             "namespace": ev["app_namespace"], "values": ev["app_values"],
+                                             "execution_id": ex.id, **({"training": run} if run else {})})
+        return res
     raise ValueError(op)
+
+
+def _check_app_params(op: str, p: dict) -> None:
+    """Release / namespace / chart end up in helm command lines: accept Kubernetes names only."""
+    chart = p.get("chart", "nginx")
+    release = p.get("release") or str(chart).split("/")[-1]
+    for what, v, rx in (("release", release, _DNS1123), ("namespace", p.get("namespace", "default"), _DNS1123),
+                        ("chart", chart, _CHART)):
+        if not isinstance(v, str) or not rx.match(v):
+            raise ValueError(f"invalid {what} {v!r}")
+    if not isinstance(p.get("values", {}) or {}, dict):
+        raise ValueError("values must be a mapping")
+    if p.get("timeout") is not None and not re.match(r"^\d+[smh]?$", str(p["timeout"])):
+        raise ValueError(f"invalid timeout {p['timeout']!r}")
+
+
+def _training_result(raw: dict) -> dict | None:
+    """Last JSON step record (tokens_per_s, step_s, loss, ...) in the collected Job log, if any."""
+    for host_tasks in (raw.get("ok") or {}).values():
+        for name, r in host_tasks.items():
+            if "collect the Job log" not in name or not isinstance(r, dict):
+                continue
+            last = None
+            for line in str(r.get("stdout", "")).splitlines():
+                line = line.strip()
+                if line.startswith("{") and "tokens_per_s" in line:
+                    try:
+                        last = json.loads(line)
+                    except ValueError:
+                        continue
+            if last is not None:
+                return last
+    return None
 
 
 def _resume_skips(ex: _Exec) -> list[str]:

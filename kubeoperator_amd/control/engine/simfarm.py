@@ -137,6 +137,12 @@ class SimFarm(FakeTransport):
             fs["/opt/kubeoperator/backup/cluster-backup.zip"] = b"PK\x05\x06" + b"\x00" * 18
             return 0, "", ""
 
+        def train_log(host, cmd, fs):
+            # simulated: shaped like the per-step JSON records rank 0 of the training chart prints
+            rec = {"step": 20, "loss": 12.16, "grad_norm": 1.0, "lr": 6e-5, "step_s": 1.645, "tokens_per_s": 19915.5,
+                   "tflops_per_gpu": 1025.1}
+            return 0, "\n".join([json.dumps(dict(rec, step=10, step_s=1.66)), json.dumps(rec)]), ""
+
         # order: later add_rule calls win (inserted first), so generic rules go first
         R(r"stat -c", fn=stat)
         R(r"ctr version", stdout="ready")
@@ -172,6 +178,8 @@ class SimFarm(FakeTransport):
         R(r"zip -qr cluster-backup.zip", fn=snapshot_zip)
         R(r"^hostname$", fn=lambda h, c, fs: (0, h, ""))
         R(r"helm version", stdout="v3.15.4+g0")
+        R(r"^helm status \S+ -n \S+ -o json", stdout="deployed")
+        R(r"kubectl -n \S+ logs -l app.kubernetes.io/instance=", fn=train_log)
         R(r"systemctl is-active", rc=3)
 
     def is_sim(self) -> bool:

@@ -104,7 +104,7 @@ def _mandatory(v):
 
 def _combine(*dicts, recursive=False):
     out = {}
-    for d in dicts:
+    for d in map(_data, dicts):
         if recursive:
             for k, v in d.items():
                 if isinstance(v, dict) and isinstance(out.get(k), dict):
@@ -122,15 +122,24 @@ def _default(value, default_value="", boolean=False):
     return value
 
 
+def _data(v):
+    """Plain data for serialising filters: lazily bound dicts / lists become dicts / lists of expanded values."""
+    if isinstance(v, dict):
+        return {k: _data(v[k]) for k in v.keys()}
+    if isinstance(v, (list, tuple)):
+        return [_data(x) for x in v]
+    return v
+
+
 FILTERS = {
     "default": _default,
     "d": _default,
     "bool": _bool,
-    "to_json": lambda v, **k: json.dumps(v, **k),
-    "to_nice_json": lambda v, indent=4: json.dumps(v, indent=indent, sort_keys=True),
+    "to_json": lambda v, **k: json.dumps(_data(v), **k),
+    "to_nice_json": lambda v, indent=4: json.dumps(_data(v), indent=indent, sort_keys=True),
     "from_json": lambda v: json.loads(v),
-    "to_yaml": lambda v, **k: yaml.safe_dump(v, default_flow_style=True).strip(),
-    "to_nice_yaml": lambda v, indent=2: yaml.safe_dump(v, default_flow_style=False, indent=indent),
+    "to_yaml": lambda v, **k: yaml.safe_dump(_data(v), default_flow_style=True).strip(),
+    "to_nice_yaml": lambda v, indent=2: yaml.safe_dump(_data(v), default_flow_style=False, indent=indent),
     "from_yaml": lambda v: yaml.safe_load(v),
     "b64encode": lambda v: base64.b64encode(str(v).encode()).decode(),
     "b64decode": lambda v: base64.b64decode(str(v).encode()).decode(),

@@ -214,7 +214,7 @@ views["cluster-create"] = async (v) => {
   $("#cc-install").onclick = () => submit(true);
 };
 
-const OPS = [["install", "Install"], ["gpu-validate", "Validate GPUs"], ["upgrade", "Upgrade"], ["scale", "Scale (IaaS)"],
+const OPS = [["install", "Install"], ["gpu-validate", "Validate GPUs"], ["app-deploy", "Deploy app"], ["upgrade", "Upgrade"], ["scale", "Scale (IaaS)"],
   ["add-worker", "Add worker"], ["remove-worker", "Remove worker"], ["backup", "Backup"], ["restore", "Restore"],
   ["bigip-config", "F5 BIG-IP"], ["uninstall", "Uninstall"]];
 
@@ -242,6 +242,7 @@ async function runOp(c, op) {
     const b = await GET(`/clusterBackup/${c.project_id}/`);
     return formModal("Restore", [["clusterBackupId", "Backup", "select", b.map((x) => [x.id, x.name])]], (d) => go(d));
   }
+  if (op === "app-deploy") { location.hash = `#/cluster/${c.name}/apps`; return; }
   if (!confirm(`${op} cluster ${c.name}?`)) return;
   await go(params);
 }
@@ -251,7 +252,7 @@ function closeSockets() { liveSockets.forEach((s) => { try { s.close(); } catch 
 
 views.cluster = async (v, [name, tab = "overview", arg]) => {
   const c = await GET(`/clusters/${name}/`);
-  const tabs = ["overview", "nodes", "deploy", "health", "events", "backup", "grade", "configs", "apps"];
+  const tabs = ["overview", "nodes", "deploy", "apps", "health", "events", "storage", "backup", "grade", "configs", "f5", "terminal"];
   v.innerHTML = `<h2>${esc(c.name)} ${st(c.status)}</h2><div class="tabs">${tabs.map((t) => `<a href="#/cluster/${esc(name)}/${t}" class="${t === tab ? "active" : ""}">${t}</a>`).join("")}</div><div id="tab"></div>`;
   const t = $("#tab");
   if (tab === "overview") {
@@ -274,8 +275,16 @@ views.cluster = async (v, [name, tab = "overview", arg]) => {
       <div><div id="steps" class="steps"></div><pre class="term" id="term"></pre></div></div>`;
     if (cur) follow(cur);
   } else if (tab === "health") {
-    const [h, hist] = await Promise.all([GET(`/cluster/${name}/health/all/`).catch((e) => ({error: e.message})), GET(`/clusterHealthHistory/${c.project_id}/`).catch(() => [])]);
-    t.innerHTML = h.error ? `<p class="muted">${esc(h.error)}</p>` : kv(h) + `<h3>Availability history</h3>` + table(hist, [["Date", "date_created"], ["Rate", "available_rate"], ["Type", "date_type"]]);
+    const [h, hist, comps, nss] = await Promise.all([GET(`/cluster/${name}/health/all/`).catch((e) => ({error: e.message})), GET(`/clusterHealthHistory/${c.project_id}/`).catch(() => []),
+      GET(`/cluster/${name}/component/`).catch(() => []), GET(`/cluster/${name}/namespace/`).catch(() => [])]);
+    t.innerHTML = `<div class="toolbar"><button id="chk" class="secondary">Check nodes</button><button id="tsk" class="secondary">Check node clocks</button></div><div id="hx"></div>` +
+      (h.error ? `<p class="muted">${esc(h.error)}</p>` : kv(h)) +
+      `<h3>Control-plane components (kube-system)</h3>${table(comps, [["Name", "name"], ["Ready", (d) => `${esc(d.ready_replicas ?? d.ready ?? "")}/${esc(d.replicas ?? "")}`], ["Status", (d) => st(d.status || "")]], "No data.")}
+       <h3>Namespaces</h3>${table(nss, [["Name", "name"], ["Status", (n) => st(n.status)]], "No data.")}
+       <h3>Availability history</h3>${table(hist, [["Date", "date_created"], ["Rate", "available_rate"], ["Type", "date_type"]])}`;
+    $("#chk").onclick = async () => { const r = await GET(`/cluster/${name}/checkNodes/`).catch((e) => ({error: e.message})); $("#hx").innerHTML = r.error ? `<p class="error">${esc(r.error)}</p>` :
+      table(Array.isArray(r) ? r : (r.nodes || []), [["Node", "name"], ["Conditions", (n) => (n.conditions || []).map((x) => st(`${x.type}:${x.status}`)).join(" ")]]); };
+    $("#tsk").onclick = async () => { const r = await GET(`/cluster/${name}/syncNodeTime/`).catch((e) => ({error: e.message})); $("#hx").innerHTML = r.error ? `<p class="error">${esc(r.error)}</p>` : kv(r); };
   } else if (tab === "events") {
     const ev = await POST(`/cluster/${name}/event/`, {limit: 200}).catch((e) => ({items: [], error: e.message}));
     t.innerHTML = table(ev.items || ev, [["Time", "last_timestamp"], ["Type", (e) => st(e.type)], ["Reason", "reason"], ["Object", "name"], ["Message", "message"]], ev.error || "No events.");
@@ -301,7 +310,60 @@ views.cluster = async (v, [name, tab = "overview", arg]) => {
       return POST(`/clusters/${name}/configs/`, {key: d.key, value: val}); });
     t.querySelectorAll("[data-del]").forEach((b) => b.onclick = () => confirmDo("Delete config?", () => DEL(`/clusters/${name}/configs/${b.dataset.del}/`)));
   } else if (tab === "apps") {
-    t.innerHTML = table(c.apps || [], [["App", "name"], ["URL", (a) => `<a href="${esc(a.url)}" target="_blank">${esc(a.url)}</a>`], ["Description", "describe"]]);
+    // Helm releases (app-deploy / app-remove executions) + the add-on links of the plan
+    const [rel, cat] = await Promise.all([GET(`/clusters/${name}/apps/`), GET("/apps/catalog/")]);
+    t.innerHTML = `<div class="toolbar"><button id="deployapp">Deploy application</button></div>
+      <h3>Releases</h3>${table(rel, [["Release", "release"], ["Namespace", "namespace"], ["Chart", "chart"], ["Deployed", "date"],
+        ["Result", (a) => a.training ? `${Math.round(a.training.tokens_per_s).toLocaleString()} tokens/s · ${esc(a.training.step_s)} s/step · loss ${esc(a.training.loss)}` : ""],
+        ["", (a) => `<a href="#/cluster/${esc(name)}/deploy/${esc(a.execution_id)}">log</a> <button class="link" data-rm="${esc(a.release)}" data-ns="${esc(a.namespace)}">remove</button>`]], "No applications deployed.")}
+      <h3>Add-on consoles</h3>${table(c.apps || [], [["App", "name"], ["URL", (a) => `<a href="${esc(a.url)}" target="_blank">${esc(a.url)}</a>`], ["Description", "describe"]])}`;
+    $("#deployapp").onclick = () => {
+      modal(`<h2>Deploy application</h2><form id="af"><label>Chart<select name="chart">${cat.map((x) => `<option value="${esc(x.name)}">${esc(x.name)} ${esc(x.version)} — ${esc(x.description)}</option>`).join("")}</select></label>
+        <div class="row"><label>Release<input name="release" placeholder="(chart name)"></label><label>Namespace<input name="namespace" value="default"></label></div>
+        <label>Values (JSON, chart defaults shown)<textarea name="values" style="min-height:260px"></textarea></label>
+        <label><input type="checkbox" name="wait_job" style="width:auto"> Wait for the Job to finish and collect its result (training chart)</label>
+        <div class="toolbar"><button type="submit">Deploy</button><button type="button" class="secondary" onclick="closeModal()">Cancel</button></div><p class="error" id="af-err"></p></form>`);
+      const f = $("#af");
+      const fill = () => { const x = cat.find((y) => y.name === f.chart.value); f.values.value = JSON.stringify(x ? x.values : {}, null, 2); f.wait_job.checked = f.chart.value === "pytorch-rocm-train"; };
+      f.chart.onchange = fill; fill();
+      f.addEventListener("submit", async (e) => {
+        e.preventDefault();
+        let values; try { values = JSON.parse(f.values.value || "{}"); } catch (err) { $("#af-err").textContent = err.message; return; }
+        const params = {chart: f.chart.value, namespace: f.namespace.value || "default", values, wait_job: f.wait_job.checked};
+        if (f.release.value) params.release = f.release.value;
+        try { const ex = await POST(`/clusters/${name}/executions/`, {operation: "app-deploy", params}); closeModal(); location.hash = `#/cluster/${name}/deploy/${ex.id}`; }
+        catch (err) { $("#af-err").textContent = err.message; }
+      });
+    };
+    t.querySelectorAll("[data-rm]").forEach((b) => b.onclick = () => confirmDo(`Remove release ${b.dataset.rm}?`, async () => {
+      const ex = await POST(`/clusters/${name}/executions/`, {operation: "app-remove", params: {release: b.dataset.rm, namespace: b.dataset.ns}});
+      location.hash = `#/cluster/${name}/deploy/${ex.id}`; }));
+  } else if (tab === "storage") {
+    const d = await GET(`/cluster/${name}/storage/`).catch((e) => ({error: e.message}));
+    t.innerHTML = d.error ? `<p class="muted">${esc(d.error)}</p>` :
+      `<h3>Storage classes</h3>${table(d.storage_classes, [["Name", (x) => esc(x.metadata.name)], ["Provisioner", "provisioner"], ["Reclaim", "reclaimPolicy"],
+        ["Default", (x) => ((x.metadata.annotations || {})["storageclass.kubernetes.io/is-default-class"] === "true" ? "yes" : "")]])}
+       <h3>Persistent volume claims</h3>${table(d.pvcs, [["Namespace", (x) => esc(x.metadata.namespace)], ["Name", (x) => esc(x.metadata.name)],
+        ["Class", (x) => esc(x.spec.storageClassName)], ["Size", (x) => esc(((x.spec.resources || {}).requests || {}).storage)], ["Phase", (x) => st((x.status || {}).phase)]])}`;
+  } else if (tab === "f5") {
+    const cfgs = Object.fromEntries((await GET(`/clusters/${name}/configs/`)).map((x) => [x.key, x.value]));
+    const keys = [["bigip_host", "BIG-IP address"], ["bigip_port", "Port"], ["bigip_user", "User"], ["bigip_password", "Password"], ["bigip_partition", "Partition"], ["bigip_public_ip", "Virtual server IP"]];
+    t.innerHTML = `<form id="f5" class="card">${keys.map(([k, l]) => `<label>${esc(l)}<input name="${k}" type="${k.includes("password") ? "password" : "text"}" value="${esc(k.includes("password") ? "" : (cfgs[k] ?? ""))}"></label>`).join("")}
+      <div class="toolbar"><button type="submit">Save &amp; configure F5</button></div><p class="error" id="f5-err"></p></form>`;
+    $("#f5").addEventListener("submit", async (e) => {
+      e.preventDefault();
+      try {
+        for (const [k] of keys) { const v = e.target.elements[k].value; if (v !== "" || !k.includes("password")) await POST(`/clusters/${name}/configs/`, {key: k, value: v}); }
+        const ex = await POST(`/clusters/${name}/executions/`, {operation: "bigip-config", params: {}});
+        location.hash = `#/cluster/${name}/deploy/${ex.id}`;
+      } catch (err) { $("#f5-err").textContent = err.message; }
+    });
+  } else if (tab === "terminal") {
+    t.innerHTML = `<p class="muted">Web terminal (webkubectl) with this cluster's kubeconfig.</p><div class="toolbar"><button id="wk">Open terminal</button>
+      <button id="tok" class="secondary">Show service-account token</button></div><pre class="term" id="wk-out" style="height:auto;min-height:60px"></pre>`;
+    $("#wk").onclick = async () => { try { const r = await GET(`/cluster/${c.name}/webkubectl/token/`); window.open(`/webkubectl/terminal/?token=${encodeURIComponent(r.token)}`, "_blank"); }
+      catch (e) { $("#wk-out").textContent = e.message; } };
+    $("#tok").onclick = async () => { try { $("#wk-out").textContent = (await GET(`/cluster/${c.name}/token/`)).token; } catch (e) { $("#wk-out").textContent = e.message; } };
   }
 };
 
@@ -432,10 +494,38 @@ views.logs = async (v) => {
   run();
 };
 
+views.profile = async (v) => {
+  v.innerHTML = `<h2>Profile</h2>${kv({username: ME.username, email: ME.email || "", superuser: ME.is_superuser, source: ME.source || "local",
+    items: (ME.item_role_mappings || []).map((m) => `${m.item_name}:${m.role}`).join(", ")})}
+    <h3>Change password</h3><form id="pw" class="card" style="max-width:420px"><label>Current password<input name="original" type="password"></label>
+    <label>New password<input name="password" type="password"></label><label>Repeat<input name="password2" type="password"></label>
+    <div class="toolbar"><button type="submit">Change</button></div><p id="pw-msg" class="muted"></p></form>`;
+  $("#pw").addEventListener("submit", async (e) => {
+    e.preventDefault();
+    const d = Object.fromEntries(new FormData(e.target).entries());
+    if (d.password !== d.password2) { $("#pw-msg").textContent = "passwords differ"; return; }
+    try { await PUT("/password/", {original: d.original, password: d.password}); $("#pw-msg").textContent = "password changed"; e.target.reset(); }
+    catch (err) { $("#pw-msg").textContent = err.message; }
+  });
+};
+
+views.training = async (v) => {
+  // the bundled PyTorch-ROCm chart: model presets and every training release across clusters
+  const [presets, cls] = await Promise.all([GET("/train/presets/"), GET("/clusters/")]);
+  const rels = (await Promise.all(cls.map((c) => GET(`/clusters/${c.name}/apps/`).then((r) => r.map((a) => ({...a, cluster: c.name}))).catch(() => []))))
+    .flat().filter((a) => a.chart === "pytorch-rocm-train");
+  v.innerHTML = `<h2>GPU training (PyTorch-ROCm chart)</h2><p class="muted">Deploy from a cluster's <i>apps</i> tab: chart <code>pytorch-rocm-train</code>, one pod per node with
+    <code>amd.com/gpu</code> × gpusPerNode, torchrun over RCCL; hand-written gfx950 kernels for attention, norms, RoPE, SwiGLU, cross-entropy and AdamW.</p>
+    <h3>Runs</h3>${table(rels, [["Cluster", (a) => `<a href="#/cluster/${esc(a.cluster)}/apps">${esc(a.cluster)}</a>`], ["Release", "release"], ["Model", (a) => esc((a.values || {}).model || "")],
+      ["GPUs/node", (a) => esc((a.values || {}).gpusPerNode || "")], ["tokens/s", (a) => a.training ? Math.round(a.training.tokens_per_s).toLocaleString() : "—"],
+      ["s/step", (a) => esc(a.training ? a.training.step_s : "")], ["TFLOP/s/GPU", (a) => esc(a.training ? a.training.tflops_per_gpu : "")], ["Date", "date"]], "No training runs yet.")}
+    <h3>Model presets</h3>${table(Object.entries(presets).map(([k, p]) => ({name: k, ...p})), [["Preset", "name"], ["Parameters", (p) => `${(p.params / 1e9).toFixed(2)} B`], ["Layers", "layers"], ["Hidden", "hidden"]])}`;
+};
+
 // ------------------------------------------------------------------ navigation
-const NAV = [["Overview", [["dashboard", "Dashboard"], ["clusters", "Clusters"]]],
+const NAV = [["Overview", [["dashboard", "Dashboard"], ["clusters", "Clusters"], ["training", "GPU training"]]],
   ["Infrastructure", [["hosts", "Hosts"], ["credentials", "Credentials"], ["regions", "Regions"], ["zones", "Zones"], ["plans", "Deploy plans"], ["packages", "Packages"], ["storage", "Storage"]]],
-  ["Administration", [["items", "Items"], ["users", "Users"], ["settings", "Settings"], ["messages", "Messages"], ["logs", "System log"]]]];
+  ["Administration", [["items", "Items"], ["users", "Users"], ["settings", "Settings"], ["messages", "Messages"], ["logs", "System log"], ["profile", "Profile"]]]];
 
 function renderNav(current) {
   $("#nav").innerHTML = NAV.map(([g, items]) => `<div class="group">${g}</div>` + items.filter(([k]) => ME.is_superuser || !["users", "settings", "credentials"].includes(k))

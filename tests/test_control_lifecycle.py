@@ -153,3 +153,35 @@ def test_unknown_operation(control):
     _cluster()
     with pytest.raises(ValueError):
         deploy.create("demo", "explode", run="none")
+
+
+def test_app_deploy_nginx_and_training_chart(control):
+    """BASELINE config #1 (deploy the nginx chart) and #3/#4 (the bundled PyTorch-ROCm training chart)
+    through ``app-deploy`` executions: helm command lines, rendered values, recorded releases, the training
+    run's last step record attached to the execution, removal, and input validation."""
+    _cluster()
+    assert deploy.create("demo", "install", run="inline")["state"] == "SUCCESS"
+    e = deploy.create("demo", "app-deploy", {"chart": "nginx", "values": {"replicas": 2}}, run="inline")
+    assert e["state"] == "SUCCESS", e["result_summary"]
+    m1 = control.farm.commands("m1")
+    helm = [c for c in m1 if c.startswith("helm upgrade --install nginx /opt/kubeoperator/charts/nginx")]
+    assert helm and "-n default --create-namespace" in helm[0] and "--wait --timeout 10m" in helm[0]
+    assert b"replicas: 2" in control.farm.fs["m1"]["/opt/kubeoperator/charts/values/nginx.yaml"]
+    assert "/opt/kubeoperator/charts/nginx/templates/deployment.yaml" in control.farm.fs["m1"]
+
+    e = deploy.create("demo", "app-deploy", {"chart": "pytorch-rocm-train", "release": "llama-8x", "namespace": "train",
+                                             "values": {"model": "llama3_8b", "gpusPerNode": 8, "steps": 20},
+                                             "wait_job": True}, run="inline")
+    assert e["state"] == "SUCCESS", e["result_summary"]
+    assert e["result_summary"]["training"]["tokens_per_s"] > 0 and e["result_summary"]["training"]["step"] == 20
+    assert any(c.startswith("kubectl -n train wait --for=condition=complete job -l app.kubernetes.io/instance=llama-8x")
+               for c in control.farm.commands("m1"))
+    apps = {a["release"]: a for a in clusters.list_apps("demo")}
+    assert set(apps) == {"nginx", "llama-8x"} and apps["llama-8x"]["training"]["tokens_per_s"] > 0
+
+    assert deploy.create("demo", "app-remove", {"release": "nginx"}, run="inline")["state"] == "SUCCESS"
+    assert [a["release"] for a in clusters.list_apps("demo")] == ["llama-8x"]
+    assert clusters.get_cluster("demo").status == "RUNNING"
+    for bad in ({"release": "x; rm -rf /"}, {"chart": "../etc"}, {"namespace": "A B"}, {"values": [1]}):
+        with pytest.raises(ValueError):
+            deploy.create("demo", "app-deploy", bad, run="none")

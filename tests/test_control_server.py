@@ -157,3 +157,25 @@ def test_operator_lifecycle_verbs(tmp_path):
     assert not list((data / "tmp").glob("*.pid"))
     r = run("uninstall", "--purge")
     assert r.returncode == 0 and not data.exists()
+
+
+def test_ui_script_parses_and_covers_the_reference_modules():
+    """The single-page UI parses (node, when present) and has a view for every reference UI module
+     plus the MI355X additions (apps / training)."""
+    import re
+    import shutil
+
+    path = os.path.join(os.path.dirname(__file__), "..", "kubeoperator_amd", "control", "ui", "app.js")
+    src = open(path).read()
+    views = set(re.findall(r"^views(?:\.|\[\")([\w-]+)", src, re.M))
+    assert {"dashboard", "clusters", "cluster-create", "cluster", "hosts", "credentials", "packages", "regions", "zones",
+            "plans", "storage", "items", "users", "settings", "messages", "logs", "profile", "training"} <= views, views
+    for tab in ("overview", "nodes", "deploy", "apps", "health", "events", "storage", "backup", "grade", "configs",
+                "f5", "terminal"):
+        assert f'tab === "{tab}"' in src or tab == "overview", tab
+    node = shutil.which("node")
+    if node:
+        r = subprocess.run([node, "--harmony-nullish", "--harmony-optional-chaining", "--check", path],
+                           capture_output=True, text=True)
+        if "bad option" not in r.stderr:
+            assert r.returncode == 0, r.stderr

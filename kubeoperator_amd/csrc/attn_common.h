@@ -179,11 +179,32 @@ __device__ __forceinline__ void dma_tile_a(char* lds, const bf16_t* src, int64_t
   }
 }
 
-// bijective XCD-aware remap of the linear block id (guide §5 "XCD swizzle must be bijective")
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  const int xcd = bid & 7, slot = bid >> 3;
-  const int q = nwg >> 3, r = nwg & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+// Work order of the attention kernels: bid -> (batch, head unit, block rank), rank 0 = the HEAVIEST block
+// under a causal mask (the kernels map rank to their query / key block). Workgroups are dispatched to the
+// 8 XCDs round-robin in bid order (bid & 7), so the order must balance the XCDs as well as the CUs:
+//   * when the L2-sharing groups (UG consecutive head units reading one K/V head) split evenly over the
+//     XCDs, XCD x runs groups x, x+8, ... -- every XCD gets the same mix of block sizes, its heads share
+//     their K/V in its L2, and inside the XCD the blocks go heaviest-first (list scheduling ~ LPT);
+//   * otherwise plain bid order, rank-major: consecutive (heavy) blocks land on different XCDs.
+// (A contiguous-chunk XCD remap of a rank-major order put all of the heaviest blocks on XCD 0: causal
+// attention ran at ~58 % of the non-causal rate, profiles/r2_attn_causal_balance.jsonl.)
+struct AttnWork {
+  int b, unit, rank;
+};
+__device__ __forceinline__ AttnWork attn_work(int bid, int B, int NU, int UG, int nblk) {
+  (void)nblk;
+  UG = UG < 1 ? 1 : UG;
+  const int G = (NU % UG == 0) ? B * (NU / UG) : 0;
+  if (G > 0 && (G & 7) == 0) {
+    const int xcd = bid & 7, s = bid >> 3;
+    const int per = (G >> 3) * UG;  // head units per XCD
+    const int rank = s / per, rem = s % per;
+    const int g = (rem / UG) * 8 + xcd;
+    const int gpb = NU / UG;  // groups per batch entry
+    return {g / gpb, (g % gpb) * UG + rem % UG, rank};
+  }
+  const int rank = bid / (B * NU), rem = bid % (B * NU);
+  return {rem / NU, rem % NU, rank};
 }
 
 }  // namespace kop

@@ -102,11 +102,9 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
   const int r = lane & 31, hh = lane >> 5;
   const int tq = (lane & 15) >> 2, tp = lane & 3, tg1 = (lane >> 4) & 1;
   const int nkb = S / BN;
-  const int nwork = B * Hq * nkb;
-  const int work = xcd_remap(blockIdx.x, nwork);
-  const int kb = work / (B * Hq);  // heaviest key blocks (earliest keys under a causal mask) first
-  const int rest = work % (B * Hq);
-  const int b = rest / Hq, hq = rest % Hq;
+  const AttnWork aw = attn_work(blockIdx.x, B, Hq, Hq / Hkv, nkb);
+  const int kb = aw.rank;  // heaviest key blocks (earliest keys under a causal mask) first
+  const int b = aw.b, hq = aw.unit;
   const int kvh = hq / (Hq / Hkv);
   const int k0 = kb * BN, k0w = k0 + 32 * wid;
   const float c2 = scale * 1.4426950408889634f;
@@ -322,11 +320,9 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dq_kernel(
   const int r = lane & 31, hh = lane >> 5;
   const int tq = (lane & 15) >> 2, tp = lane & 3, tg1 = (lane >> 4) & 1;
   const int nqb = S / BM;
-  const int nwork = B * Hq * nqb;
-  const int work = xcd_remap(blockIdx.x, nwork);
-  const int qb = causal ? (nqb - 1 - work / (B * Hq)) : work / (B * Hq);
-  const int rest = work % (B * Hq);
-  const int b = rest / Hq, hq = rest % Hq;
+  const AttnWork aw = attn_work(blockIdx.x, B, Hq, Hq / Hkv, nqb);
+  const int qb = causal ? (nqb - 1 - aw.rank) : aw.rank;
+  const int b = aw.b, hq = aw.unit;
   const int kvh = hq / (Hq / Hkv);
   const int q0 = qb * BM, q0w = q0 + wid * 32;
   const int ntiles = causal ? (q0 + BM) / BN : S / BN;
@@ -471,11 +467,9 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq8_kernel(
   const int tq = (lane & 15) >> 2, tp = lane & 3, tg1 = (lane >> 4) & 1;
   const bool late = STAGGER && wid >= 4;
   const int nqb = S / BM;
-  const int nwork = B * Hq * nqb;
-  const int work = xcd_remap(blockIdx.x, nwork);
-  const int qb = causal ? (nqb - 1 - work / (B * Hq)) : work / (B * Hq);
-  const int rest = work % (B * Hq);
-  const int b = rest / Hq, hq = rest % Hq;
+  const AttnWork aw = attn_work(blockIdx.x, B, Hq, Hq / Hkv, nqb);
+  const int qb = causal ? (nqb - 1 - aw.rank) : aw.rank;
+  const int b = aw.b, hq = aw.unit;
   const int kvh = hq / (Hq / Hkv);
   const int q0 = qb * BM, q0w = q0 + wid * 32;
   const int ntiles = causal ? (q0 + BM) / BN : S / BN;
@@ -664,11 +658,9 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __re
   const int r = lane & 31, hh = lane >> 5;
   const int tq = (lane & 15) >> 2, tp = lane & 3, tg1 = (lane >> 4) & 1;
   const int ngrp = Hq / HP, nqb = S / RH;
-  const int nwork = B * ngrp * nqb;
-  const int work = xcd_remap(blockIdx.x, nwork);
-  const int qb = causal ? (nqb - 1 - work / (B * ngrp)) : work / (B * ngrp);
-  const int rest = work % (B * ngrp);
-  const int b = rest / ngrp, hg = rest % ngrp;
+  const AttnWork aw = attn_work(blockIdx.x, B, ngrp, (Hq / Hkv) / HP, nqb);
+  const int qb = causal ? (nqb - 1 - aw.rank) : aw.rank;
+  const int b = aw.b, hg = aw.unit;
   const int kvh = (hg * HP) / (Hq / Hkv);
   const int hq = hg * HP + wid / WPH;  // this wave's head
   const int q0 = qb * RH, q0w = q0 + 32 * (wid % WPH);

@@ -46,11 +46,9 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_fwd_kernel(const bf16_t* __rest
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   const int nqb = S / BM;
-  const int nwork = B * Hq * nqb;
-  const int work = xcd_remap(blockIdx.x, nwork);
-  const int qb = causal ? (nqb - 1 - work / (B * Hq)) : work / (B * Hq);
-  const int rest = work % (B * Hq);
-  const int b = rest / Hq, hq = rest % Hq;
+  const AttnWork aw = attn_work(blockIdx.x, B, Hq, Hq / Hkv, nqb);
+  const int qb = causal ? (nqb - 1 - aw.rank) : aw.rank;
+  const int b = aw.b, hq = aw.unit;
   const int kvh = hq / (Hq / Hkv);
   const int q0 = qb * BM, q0w = q0 + wid * 32;
   const int ntiles = causal ? (q0 + BM) / BN : S / BN;
@@ -238,11 +236,9 @@ __global__ void __launch_bounds__(512, 1) fa_fwd8_kernel(const bf16_t* __restric
   const int r = lane & 31, hh = lane >> 5;
   const bool late = STAGGER && wid >= 4;
   const int nqb = S / BM;
-  const int nwork = B * Hq * nqb;
-  const int work = xcd_remap(blockIdx.x, nwork);
-  const int qb = causal ? (nqb - 1 - work / (B * Hq)) : work / (B * Hq);
-  const int rest = work % (B * Hq);
-  const int b = rest / Hq, hq = rest % Hq;
+  const AttnWork aw = attn_work(blockIdx.x, B, Hq, Hq / Hkv, nqb);
+  const int qb = causal ? (nqb - 1 - aw.rank) : aw.rank;
+  const int b = aw.b, hq = aw.unit;
   const int kvh = hq / (Hq / Hkv);
   const int q0 = qb * BM, q0w = q0 + wid * 32;
   const int ntiles = causal ? (q0 + BM) / BN : S / BN;

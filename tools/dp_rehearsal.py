@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--accum", type=int, default=1, help="gradient-accumulation micro-batches per step")
     ap.add_argument("--bucket-mb", type=int, default=1)
+    ap.add_argument("--grad-dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--lr", type=float, default=1e-1, help="large, so a missing or double update is visible")
     ap.add_argument("--eps", type=float, default=1.0,
                     help="Adam eps >> |grad|: the update is ~linear in the gradient instead of +-lr per element, so "
@@ -49,7 +50,7 @@ def main():
     info = init_distributed("cuda" if torch.cuda.is_available() else "cpu")
     world, rank = info.world, info.rank
     kw = dict(model=a.model, seq_len=a.seq, warmup_steps=1, total_steps=10, bucket_mb=a.bucket_mb,
-              overlap_optimizer=True, lr=a.lr, eps=a.eps)
+              overlap_optimizer=True, lr=a.lr, eps=a.eps, grad_dtype=a.grad_dtype)
     tr = Trainer(TrainConfig(micro_batch=a.mbs, grad_accum=a.accum, dp_mode=a.mode, **kw), info)
     init = flat(tr)
     sl = slice(a.mbs * rank, a.mbs * (rank + 1))

@@ -5,12 +5,13 @@ set -o pipefail
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 port=29560
-for cfg in "2 zero1 1" "2 allreduce 1" "4 zero1 1" "4 allreduce 1" "2 zero1 2" "4 zero1 4"; do
+for cfg in "2 zero1 1 bf16" "2 allreduce 1 bf16" "4 zero1 1 bf16" "4 allreduce 1 bf16" "2 zero1 2 bf16" \
+           "4 zero1 4 bf16" "4 zero1 4 fp32" "2 allreduce 2 fp32"; do
   set -- $cfg
   port=$((port + 1))
   timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node $1 --master-addr 127.0.0.1 \
-    --master-port $port tools/dp_rehearsal.py --mode $2 --accum $3 > gpurun_out/dp_$1_$2_a$3.log 2>&1
-  rc=$?; echo "dp$1 $2 accum$3 rc=$rc $(grep rehearsal gpurun_out/dp_$1_$2_a$3.log)"; [ $rc -eq 0 ] || exit $rc
+    --master-port $port tools/dp_rehearsal.py --mode $2 --accum $3 --grad-dtype $4 > gpurun_out/dp_$1_$2_a$3_$4.log 2>&1
+  rc=$?; echo "dp$1 $2 accum$3 $4 rc=$rc $(grep rehearsal gpurun_out/dp_$1_$2_a$3_$4.log)"; [ $rc -eq 0 ] || exit $rc
 done
 # Llama-3 1B proxy (vocab 128256, hidden 2048) with the production 512 MiB buckets
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \

@@ -29,7 +29,16 @@ def setup(mode: str = "use", path: str | None = None, rank: int = 0) -> str:
     if mode == "use" and not os.path.exists(path):
         return "off (no tuned results)"
     tun.enable(True)
-    tun.set_filename(path, insert_device_ordinal=False)
+    if mode == "use":
+        # winners are only READ here. Some torch versions rewrite TunableOp's output file at process exit:
+        # point that file at a per-rank scratch path so the ranks of a multi-GPU job (and back-to-back jobs
+        # reading the committed winners) never race on or rewrite the shared results file
+        import tempfile
+
+        tun.set_filename(os.path.join(tempfile.gettempdir(), f"kop_tunableop_rank{rank}.csv"),
+                         insert_device_ordinal=False)
+    else:
+        tun.set_filename(path, insert_device_ordinal=False)
     if mode == "tune":
         os.makedirs(os.path.dirname(path), exist_ok=True)
         tun.tuning_enable(True)

@@ -6,9 +6,16 @@ ranks hold identical state but each writes its own file so resume never needs cr
 rank has written (rank 0 writes the marker after a barrier), so a crash mid-save resumes from the
 previous complete checkpoint. Files are written to a temp name and renamed (atomic on POSIX).
 Loading uses ``torch.load(weights_only=True)``: checkpoints are tensors + plain containers only.
+
+Elastic resume: a job restarted on a different number of GPUs (a node lost GPUs, or more were added) loads
+a checkpoint written at another world size. Every file carries its flat layout (parameter offsets, and
+where each optimizer-state segment sits); the loader memory-maps the old ranks' files and copies, per
+parameter, the intersection of the old pieces with this rank's new segments -- each rank reads only its own
+new shard of the fp32 state (12 B/param / world), never the whole 96 GB of an 8B model.
 """
 from __future__ import annotations
 
+import bisect
 import os
 
 import torch
@@ -43,13 +50,88 @@ def latest_step(directory: str):
         return int(f.read().strip())
 
 
+def _files(d: str) -> list[str]:
+    ranks = sorted(int(f[5:-3]) for f in os.listdir(d) if f.startswith("rank_") and f.endswith(".pt"))
+    return [os.path.join(d, f"rank_{r}.pt") for r in ranks]
+
+
 def load(trainer, directory: str, info: DistInfo, step: int | None = None) -> int | None:
     step = latest_step(directory) if step is None else step
     if step is None:
         return None
-    path = os.path.join(directory, f"step_{step}", f"rank_{info.rank}.pt")
-    sd = torch.load(path, map_location=info.device, weights_only=True)
-    trainer.load_state_dict(sd)
+    d = os.path.join(directory, f"step_{step}")
+    files = _files(d)
+    own = os.path.join(d, f"rank_{info.rank}.pt")
+    head = torch.load(files[0], map_location="cpu", weights_only=True, mmap=True)
+    same = head["world"] == info.world and head["params"].numel() == trainer.store.params.numel()
+    if same:
+        sd = torch.load(own, map_location=info.device, weights_only=True)
+        trainer.load_state_dict(sd)
+    else:
+        _reshard(trainer, head, files)
+        sd = torch.load(own, map_location="cpu", weights_only=True, mmap=True) if os.path.exists(own) else head
     if "rng_cpu" in sd:
         torch.set_rng_state(sd["rng_cpu"].cpu())
     return step
+
+
+def _intersect(a0, a1, b0, b1):
+    lo, hi = max(a0, b0), min(a1, b1)
+    return (lo, hi) if lo < hi else None
+
+
+@torch.no_grad()
+def _reshard(trainer, head: dict, files: list[str]) -> None:
+    """Load a checkpoint written at another world size into this rank's layout."""
+    if "layout" not in head:
+        raise ValueError("checkpoint predates layout metadata: resume with the world size that wrote it")
+    st, opt = trainer.store, trainer.opt
+    st.await_all()
+    old = head["layout"]
+    old_at = {n: (o, k) for n, o, k in zip(old["names"], old["offsets"], old["numels"])}
+    new = trainer.layout()
+    missing = set(new["names"]) - set(old_at)
+    if missing:
+        raise ValueError(f"checkpoint lacks parameters {sorted(missing)[:5]}")
+    # parameters: replicated, taken from the first file
+    for name, p in st.named_params():
+        o, k = old_at[name]
+        p.data.view(-1).copy_(head["params"][o:o + k].to(p.device))
+    # optimizer state: old pieces (any rank's file) -> this rank's segments, per parameter
+    params = [(st.offsets[n], old_at[n][0], old_at[n][1]) for n in new["names"]]  # (new off, old off, numel)
+    for buf in ("master", "exp_avg", "exp_avg_sq"):
+        getattr(opt, buf).zero_()
+    new_p = sorted(new["pieces"])
+    new_starts = [x[0] for x in new_p]
+    for f in files:
+        sd = head if f == files[0] else torch.load(f, map_location="cpu", weights_only=True, mmap=True)
+        osd = sd["optimizer"]
+        old_p = sorted(sd["layout"]["pieces"])
+        old_starts = [x[0] for x in old_p]
+        for (noff, ooff, k) in params:
+            # pieces overlapping the parameter in each layout (pieces are disjoint, sorted by start)
+            olds = old_p[max(0, bisect.bisect_right(old_starts, ooff) - 1):bisect.bisect_left(old_starts, ooff + k)]
+            news = new_p[max(0, bisect.bisect_right(new_starts, noff) - 1):bisect.bisect_left(new_starts, noff + k)]
+            for (oa, oe, om) in olds:
+                a = _intersect(ooff, ooff + k, oa, oe)  # param indices held by this old piece (old coords)
+                if a is None:
+                    continue
+                for (na, ne, nm) in news:
+                    b = _intersect(noff, noff + k, na, ne)  # param indices this new segment needs
+                    if b is None:
+                        continue
+                    c = _intersect(a[0] - ooff, a[1] - ooff, b[0] - noff, b[1] - noff)
+                    if c is None:
+                        continue
+                    src = om + (ooff + c[0] - oa)
+                    dst = nm + (noff + c[0] - na)
+                    n = c[1] - c[0]
+                    for buf in ("master", "exp_avg", "exp_avg_sq"):
+                        getattr(opt, buf)[dst:dst + n].copy_(osd[buf][src:src + n])
+        if f != files[0]:
+            del sd
+    opt.step_count = int(head["optimizer"]["step"])
+    # bf16 parameters follow the fp32 masters of this rank's segments (identical values: they were rounded
+    # from the same masters), and the transposed weight copies follow the parameters
+    st.refresh_transposed()
+    trainer.step = int(head["step"])

@@ -142,15 +142,27 @@ class Trainer:
         return self._graph_loss[key].clone()
 
     # checkpoint -----------------------------------------------------------------------------------
+    def layout(self) -> dict:
+        """Where every parameter and every optimizer-state segment lives in the flat buffers (they depend on
+        the world size through bucket padding): what checkpoint resharding maps through."""
+        st = self.store
+        names = [n for n, _ in st.named_params()]
+        base, es = st.params.data_ptr(), st.params.element_size()
+        pieces = [((sg.param.data_ptr() - base) // es, (sg.param.data_ptr() - base) // es + (b - a), a)
+                  for sg, (a, b) in zip(self.opt.segments, self.opt._views)]
+        return {"names": names, "offsets": [st.offsets[n] for n in names],
+                "numels": [st.param(n).numel() for n in names], "numel": st.numel, "pieces": pieces}
+
     def state_dict(self):
         self.store.await_all()
         return {"step": self.step, "train_config": self.tc.to_dict(), "model_config": self.cfg.to_dict(),
                 "params": self.store.params, "optimizer": self.opt.state_dict(), "world": self.info.world,
-                "rank": self.info.rank, "dp_mode": self.tc.dp_mode}
+                "rank": self.info.rank, "dp_mode": self.tc.dp_mode, "layout": self.layout()}
 
     def load_state_dict(self, sd):
-        if sd["world"] != self.info.world and self.tc.dp_mode == "zero1":
-            raise ValueError("ZeRO-1 checkpoints are sharded per rank: resume with the same world size")
+        """Same world size and layout: direct copy. (Other world sizes: ``checkpoint.load`` reshards.)"""
+        if sd["world"] != self.info.world or sd["params"].numel() != self.store.params.numel():
+            raise ValueError("checkpoint layout differs from this run's: load it through checkpoint.load")
         self.store.await_all()
         self.store.params.copy_(sd["params"])
         self.opt.load_state_dict(sd["optimizer"])

@@ -289,3 +289,43 @@ def test_monitor_with_stub_clients(control):
     assert ok["status"] == "True"
     monitor.record_availability("mon", 99.0)
     assert monitor.availability_history(clusters.get_cluster("mon").id)[0]["available_rate"] == 99.0
+
+
+def test_monitoring_content_matches_exported_metrics():
+    """Grafana dashboards, alert rules and the NPD GPU monitor shipped by the cluster-addon role: valid JSON /
+    YAML, and every training series they query is one the training chart's exporter defines."""
+    import json
+    import re
+
+    import yaml
+
+    from kubeoperator_amd.control.domain.plan import PLAYBOOK_DIR
+    from kubeoperator_amd.control.engine.templating import render_text
+
+    role = os.path.join(PLAYBOOK_DIR, "roles", "cluster-addon")
+    src = open(os.path.join(os.path.dirname(PLAYBOOK_DIR), "..", "..", "train", "metrics.py")).read()
+    exported = set(re.findall(r'"(kop_train_[a-z_]+)"', src))
+    queried = set()
+    for name in ("amd-gpu.json", "training.json", "cluster.json"):
+        d = json.load(open(os.path.join(role, "files", "dashboards", name)))
+        assert d["uid"].startswith("kop-") and d["panels"]
+        for p in d["panels"]:
+            for t in p["targets"]:
+                queried |= set(re.findall(r"kop_train_[a-z_]+", t["expr"]))
+    vals = yaml.safe_load(render_text(open(os.path.join(role, "templates", "prometheus-values.yaml.j2")).read(),
+                                      {"prometheus_retention_days": 7, "APP_DOMAIN": "apps.example"}))
+    rules = [r for g in vals["serverFiles"]["alerting_rules.yml"]["groups"] for r in g["rules"]]
+    names = {r["alert"] for r in rules}
+    assert {"TargetDown", "ContainerMemoryHigh", "GPUUncorrectableECC", "GPUUnhealthy", "TrainingStalled"} <= names
+    for r in rules:
+        queried |= set(re.findall(r"kop_train_[a-z_]+", r["expr"]))
+    assert "{{ $labels" in open(os.path.join(role, "templates", "prometheus-values.yaml.j2")).read().replace(
+        "{% raw %}", "")
+    exported_series = exported | {f"{m}_total" for m in exported}
+    assert queried and queried <= exported_series, queried - exported_series
+    npd = yaml.safe_load(render_text(open(os.path.join(role, "templates", "npd-values.yaml.j2")).read(), {}))
+    mon = json.loads(npd["settings"]["custom_monitor_definitions"]["amdgpu-monitor.json"])
+    assert mon["conditions"][0]["type"] == "AMDGPUProblem"
+    for rule in mon["rules"]:
+        re.compile(rule["pattern"])
+    assert re.search(mon["rules"][0]["pattern"], "[drm:amdgpu_job_timedout [amdgpu]] *ERROR* ring gfx_0.0.0 timeout")

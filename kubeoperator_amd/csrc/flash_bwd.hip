@@ -161,7 +161,12 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
   // the previous stage's dS stores are this wave's 16 youngest vector-memory ops: they may stay in flight
   // across the barrier (only this stage's DMA, issued before them, must have landed)
   bool stored = false;
-  for (int qt = qt0; qt < nqt; ++qt) {
+  // the causal mask is needed only in the workgroup's diagonal region (its first BN/BQ = NW query stages):
+  // the stage body is instantiated twice -- masked for those stages, mask-free for the rest -- so the 32
+  // compare/select VALU per stage (~1 per MFMA in this VALU-issue-bound loop) leave the steady state
+  // (two loops, not a branch in one body: a branch merged the live ranges and spilled)
+  auto body = [&](int qt, auto mask_c) {
+    constexpr bool MASK = decltype(mask_c)::value;
     const int stage = (qt - qt0) & 1;
     if (WDS && stored) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -214,11 +219,14 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
       }
       const int key = k0w + r;
       // key > query  <=>  kd > (j & 3) + 8 * (j >> 2): one subtraction, then compares with constants
-      const int kd = causal ? key - qs0 - 4 * hh : -1;
+      const int kd = key - qs0 - 4 * hh;
+      (void)kd;
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         float p = __builtin_amdgcn_exp2f(sacc[j] * c2);
-        if (kd > (j & 3) + 8 * (j >> 2)) p = 0.f;
+        if constexpr (MASK) {
+          if (kd > (j & 3) + 8 * (j >> 2)) p = 0.f;
+        }
         sacc[j] = p;
         dpacc[j] = p * dpacc[j];
       }
@@ -267,7 +275,13 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
       });
     }
     asm volatile("" ::: "memory");
+  };
+  int qt = qt0;
+  if (causal) {
+    const int qd = qt0 + NW < nqt ? qt0 + NW : nqt;
+    for (; qt < qd; ++qt) body(qt, std::true_type{});
   }
+  for (; qt < nqt; ++qt) body(qt, std::false_type{});
   if constexpr (DIRECT) {
     bf16_t* dkb = reinterpret_cast<bf16_t*>(dk_part) + (int64_t)(b * S + k0w + r) * dks + hq * D;
     bf16_t* dvb = reinterpret_cast<bf16_t*>(dv_part) + (int64_t)(b * S + k0w + r) * dvs + hq * D;
@@ -855,13 +869,14 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
   if (use_ds(B, S, Hq)) {
     bf16_t* ds = reinterpret_cast<bf16_t*>(ndelta + T * Hq);
     const bool direct = Hq == Hkv;
+    const int cflag = causal ? 1 : 0;
     if (direct)
       fa_bwd_dkdv_kernel<D, NW, true, true><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(
           q, k, v, dout, nlse, ndelta, reinterpret_cast<float*>(dk), reinterpret_cast<float*>(dv), ds, B, S, Hq, Hkv,
-          qs, ks, vs, dos, scale, causal, dks, dvs);
+          qs, ks, vs, dos, scale, cflag, dks, dvs);
     else
       fa_bwd_dkdv_kernel<D, NW, true><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(
-          q, k, v, dout, nlse, ndelta, dk_part, dv_part, ds, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);
+          q, k, v, dout, nlse, ndelta, dk_part, dv_part, ds, B, S, Hq, Hkv, qs, ks, vs, dos, scale, cflag);
     const int grp = Hq / Hkv;  // heads per workgroup: largest power of two dividing the GQA group, <= 8
     const int hp = (grp % 8 == 0) ? 8 : (grp % 4 == 0) ? 4 : (grp % 2 == 0) ? 2 : 1;
     if (hp == 8) launch_dq_ds<D, 8>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);

@@ -80,8 +80,11 @@ __device__ __forceinline__ int ds_slot(int key) {
 
 // DIRECT (no GQA, Hq == Hkv): the workgroup's sums are already the final dK / dV, written as bf16 straight
 // into dk_part / dv_part reinterpreted as the bf16 outputs (row strides dks / dvs), with no finalize pass.
-template <int D, int NW, bool WDS = false, bool DIRECT = false>
-__global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
+// NW waves x 32 keys per workgroup; NSTAGE-deep ring of query stages (prefetch distance NSTAGE - 1).
+// NW = 4: two workgroups per CU; NW = 8: one 512-thread workgroup per CU (each staged Q/dO tile then serves
+// 256 keys, and the LDS left over holds a 3-deep ring).
+template <int D, int NW, bool WDS = false, bool DIRECT = false, int NSTAGE = 2>
+__global__ void __launch_bounds__(NW * 64, (NW >= 8 ? 1 : 2)) fa_bwd_dkdv_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ nlse, const float* __restrict__ ndelta,
     float* __restrict__ dk_part, float* __restrict__ dv_part, bf16_t* __restrict__ ds, int B, int S, int Hq,
@@ -95,6 +98,7 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
   constexpr int STAGE = 2 * QT + 1024;           // Q, dO, {lse[32], delta[32]} piece
   constexpr int MYP = (2 * QT / 1024) / NW;      // Q/dO DMA pieces per wave per stage
   static_assert(MYP * NW * 1024 == 2 * QT, "stage must split evenly over the waves");
+  static_assert(NSTAGE == 2 || NSTAGE == 3, "2- or 3-deep stage ring");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const Kl = smem;
 
@@ -133,6 +137,9 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
   // K block of the workgroup -> LDS (counted with the first stage)
   dma_tile_a<ROWB, NW, BN>(Kl, k + (int64_t)(b * S + k0) * ks + kvh * D, ks, wid, lane);
   issue(qt0, 0);
+  if constexpr (NSTAGE == 3) {
+    if (qt0 + 1 < nqt) issue(qt0 + 1, 1);
+  }
   // lane bases of the sub-tiled images (swza): row reads of rows r (+32*i) at chunk 2kk+hh, transposed
   // reads of rows R0 + 4hh + tq
   constexpr int RB = ROWB * 8;
@@ -167,13 +174,30 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_kernel(
   // (two loops, not a branch in one body: a branch merged the live ranges and spilled)
   auto body = [&](int qt, auto mask_c) {
     constexpr bool MASK = decltype(mask_c)::value;
-    const int stage = (qt - qt0) & 1;
-    if (WDS && stored) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int stage = (qt - qt0) % NSTAGE;
+    if constexpr (NSTAGE == 2) {
+      if (WDS && stored) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      // in flight, oldest first: ..., DMA(qt), [stores(qt-2)], DMA(qt+1), [stores(qt-1)]: wait until only
+      // DMA(qt+1) and the previous stage's stores may remain (everything older, DMA(qt) included, landed)
+      const bool nxt = qt + 1 < nqt;
+      const bool st = WDS && stored;
+      if (!nxt) {
+        if (st) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if (wid == 0) {  // wave 0 also issues the lse / delta piece
+        if (st) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MYP + 1 + 16) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MYP + 1) : "memory");
+      } else {
+        if (st) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MYP + 16) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MYP) : "memory");
+      }
+    }
     stored = false;
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (qt + 1 < nqt) issue(qt + 1, stage ^ 1);
+    if (qt + NSTAGE - 1 < nqt) issue(qt + NSTAGE - 1, (qt + NSTAGE - 1 - qt0) % NSTAGE);
     const char* Ql = smem + KB + stage * STAGE;
     const char* Ol = Ql + QT;
     const float* LD = reinterpret_cast<const float*>(Ql + 2 * QT);
@@ -836,6 +860,31 @@ size_t flash_attn_bwd_workspace(int B, int S, int Hq, int D) {
   return (size_t)B * S * Hq * D * 4 * 2 + (size_t)B * Hq * S * 4 * 3 + (use_ds(B, S, Hq) ? ds_bytes(B, S, Hq) : 0);
 }
 
+// dK/dV kernel with the dS stores (variant 10): workgroup shape W waves x 32 keys, NS-deep stage ring
+template <int D, int W, int NS>
+static void launch_dkdv_ds(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout, const float* nlse,
+                           const float* ndelta, float* dk_part, float* dv_part, bf16_t* dk, bf16_t* dv, bf16_t* ds,
+                           int B, int S, int Hq, int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t dos, int64_t dks,
+                           int64_t dvs, float scale, int causal, hipStream_t stream) {
+  const size_t lds = 32 * W * (D * 2) + NS * (2 * 32 * (D * 2) + 1024);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)fa_bwd_dkdv_kernel<D, W, true, false, NS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)fa_bwd_dkdv_kernel<D, W, true, true, NS>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  const dim3 grid(B * Hq * (S / (32 * W)));
+  if (Hq == Hkv)  // no GQA: bf16 dK / dV straight from the kernel
+    fa_bwd_dkdv_kernel<D, W, true, true, NS><<<grid, W * 64, lds, stream>>>(
+        q, k, v, dout, nlse, ndelta, reinterpret_cast<float*>(dk), reinterpret_cast<float*>(dv), ds, B, S, Hq, Hkv,
+        qs, ks, vs, dos, scale, causal, dks, dvs);
+  else
+    fa_bwd_dkdv_kernel<D, W, true, false, NS><<<grid, W * 64, lds, stream>>>(
+        q, k, v, dout, nlse, ndelta, dk_part, dv_part, ds, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);
+}
+
 template <int D>
 static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
                        const float* lse, bf16_t* dq, bf16_t* dk, bf16_t* dv, void* workspace, int B, int S, int Hq,
@@ -869,14 +918,26 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
   if (use_ds(B, S, Hq)) {
     bf16_t* ds = reinterpret_cast<bf16_t*>(ndelta + T * Hq);
     const bool direct = Hq == Hkv;
+    static const int cfg = [] {
+      const char* e = getenv("KOP_DKDV_CFG");  // 42: 4 waves / 2-deep ring (2 workgroups per CU); 83, 82
+      return e ? atoi(e) : 42;
+    }();
     const int cflag = causal ? 1 : 0;
-    if (direct)
-      fa_bwd_dkdv_kernel<D, NW, true, true><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(
-          q, k, v, dout, nlse, ndelta, reinterpret_cast<float*>(dk), reinterpret_cast<float*>(dv), ds, B, S, Hq, Hkv,
-          qs, ks, vs, dos, scale, cflag, dks, dvs);
-    else
-      fa_bwd_dkdv_kernel<D, NW, true><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(
-          q, k, v, dout, nlse, ndelta, dk_part, dv_part, ds, B, S, Hq, Hkv, qs, ks, vs, dos, scale, cflag);
+    bool done = false;
+    if constexpr (D == 128) {  // 8 waves need >= 8 1-KiB pieces per Q / dO tile (32 rows x 256 B)
+      if (cfg == 83 && S % 256 == 0) {
+        launch_dkdv_ds<D, 8, 3>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks,
+                                vs, dos, dks, dvs, scale, cflag, stream);
+        done = true;
+      } else if (cfg == 82 && S % 256 == 0) {
+        launch_dkdv_ds<D, 8, 2>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks,
+                                vs, dos, dks, dvs, scale, cflag, stream);
+        done = true;
+      }
+    }
+    if (!done)
+      launch_dkdv_ds<D, NW, 2>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs,
+                               dos, dks, dvs, scale, cflag, stream);
     const int grp = Hq / Hkv;  // heads per workgroup: largest power of two dividing the GQA group, <= 8
     const int hp = (grp % 8 == 0) ? 8 : (grp % 4 == 0) ? 4 : (grp % 2 == 0) ? 2 : 1;
     if (hp == 8) launch_dq_ds<D, 8>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);

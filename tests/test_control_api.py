@@ -192,3 +192,30 @@ def test_prometheus_metrics(client, control):
     assert 'kubeoperator_step_seconds_count{operation="install",status="success",step="master"}' in text
     assert 'kubeoperator_clusters{status="RUNNING"} 1.0' in text
     assert 'kubeoperator_gpus{model="AMD Instinct MI355X"}' in text
+
+
+def test_app_catalog_and_deploy_over_http(client):
+    """Bundled chart catalog, app-deploy execution over REST (validated names), recorded releases."""
+    from kubeoperator_amd.control.runtime import jobs
+
+    cat = {c["name"]: c for c in client.get("/api/v1/apps/catalog/").json()}
+    assert {"nginx", "pytorch-rocm-train"} <= set(cat)
+    assert cat["pytorch-rocm-train"]["values"]["model"] == "llama3_8b"
+    _register_hosts(client)
+    client.post("/api/v1/clusters/", json={
+        "name": "demo", "template": "single-master", "item_name": "KubeOperator",
+        "nodes": [{"name": "m1", "host": "m1", "roles": ["master"]}, {"name": "w1", "host": "w1", "roles": ["worker"]}]})
+    eid = client.post("/api/v1/clusters/demo/executions/", json={"operation": "install"}).json()["id"]
+    jobs.run_job(jobs._claim_specific(eid))
+    r = client.post("/api/v1/clusters/demo/executions/",
+                    json={"operation": "app-deploy", "params": {"chart": "nginx", "release": "Bad Name"}})
+    assert r.status_code == 400
+    r = client.post("/api/v1/clusters/demo/executions/",
+                    json={"operation": "app-deploy", "params": {"chart": "pytorch-rocm-train", "release": "gpt2",
+                                                                "values": {"model": "gpt2_small"}, "wait_job": True}})
+    assert r.status_code == 201, r.text
+    jobs.run_job(jobs._claim_specific(r.json()["id"]))
+    e = client.get(f"/api/v1/clusters/demo/executions/{r.json()['id']}/").json()
+    assert e["state"] == "SUCCESS" and e["result_summary"]["training"]["tokens_per_s"] > 0
+    apps = client.get("/api/v1/clusters/demo/apps/").json()
+    assert [a["release"] for a in apps] == ["gpt2"] and apps[0]["values"]["model"] == "gpt2_small"

@@ -301,8 +301,11 @@ def _dispatch(ex: _Exec, c: M.Cluster, ev: dict) -> dict:
     if op in ("app-deploy", "app-remove"):
         p = ex.params
         chart = p.get("chart", "nginx")
+        from ..engine.templating import mark_unsafe
+
+        # the values are user data written to a file: never evaluated as templates
         ev.update(app_chart=chart, app_release=p.get("release") or chart.split("/")[-1],
-                  app_namespace=p.get("namespace", "default"), app_values=p.get("values") or {},
+                  app_namespace=p.get("namespace", "default"), app_values=mark_unsafe(p.get("values") or {}),
                   app_wait_job=bool(p.get("wait_job", False)))
         if p.get("timeout"):
             ev["app_timeout"] = str(p["timeout"])
@@ -313,7 +316,7 @@ def _dispatch(ex: _Exec, c: M.Cluster, ev: dict) -> dict:
             if run:
                 res["summary"]["training"] = run
             clusters.record_app(c.name, op, {"release": ev["app_release"], "chart": chart,
-                                             "namespace": ev["app_namespace"], "values": ev["app_values"],
+                                             "namespace": ev["app_namespace"], "values": p.get("values") or {},
                                              "execution_id": ex.id, **({"training": run} if run else {})})
         return res
     raise ValueError(op)

@@ -124,8 +124,10 @@ def _default(value, default_value="", boolean=False):
 
 def _data(v):
     """Plain data for serialising filters: lazily bound dicts / lists become dicts / lists of expanded values."""
+    if isinstance(v, Unsafe):
+        return str.__str__(v)
     if isinstance(v, dict):
-        return {k: _data(v[k]) for k in v.keys()}
+        return {_data(k): _data(v[k]) for k in v.keys()}
     if isinstance(v, (list, tuple)):
         return [_data(x) for x in v]
     return v
@@ -180,6 +182,22 @@ TESTS = {
 
 class TemplateRecursionError(TemplateError):
     pass
+
+
+class Unsafe(str):
+    """A string that is data, never a template (Ansible's ``!unsafe``): user content such as Helm values
+    is wrapped in it so ``{{ ... }}`` inside it is written out literally instead of being evaluated."""
+
+
+def mark_unsafe(value):
+    """Recursively wrap the strings of a JSON-like value in :class:`Unsafe`."""
+    if isinstance(value, str):
+        return Unsafe(value)
+    if isinstance(value, dict):
+        return {mark_unsafe(k): mark_unsafe(v) for k, v in value.items()}
+    if isinstance(value, (list, tuple)):
+        return [mark_unsafe(v) for v in value]
+    return value
 
 
 _MAX_DEPTH = 16
@@ -275,7 +293,7 @@ def _plain(variables) -> dict:
 
 
 def has_template(s) -> bool:
-    return isinstance(s, str) and ("{{" in s or "{%" in s)
+    return isinstance(s, str) and not isinstance(s, Unsafe) and ("{{" in s or "{%" in s)
 
 
 def render(value, variables: dict):

@@ -162,12 +162,14 @@ def test_app_deploy_nginx_and_training_chart(control):
     run's last step record attached to the execution, removal, and input validation."""
     _cluster()
     assert deploy.create("demo", "install", run="inline")["state"] == "SUCCESS"
-    e = deploy.create("demo", "app-deploy", {"chart": "nginx", "values": {"replicas": 2}}, run="inline")
+    e = deploy.create("demo", "app-deploy", {"chart": "nginx", "values": {"replicas": 2, "note": "{{ inventory_hostname }}"}},
+                      run="inline")
     assert e["state"] == "SUCCESS", e["result_summary"]
     m1 = control.farm.commands("m1")
     helm = [c for c in m1 if c.startswith("helm upgrade --install nginx /opt/kubeoperator/charts/nginx")]
     assert helm and "-n default --create-namespace" in helm[0] and "--wait --timeout 10m" in helm[0]
-    assert b"replicas: 2" in control.farm.fs["m1"]["/opt/kubeoperator/charts/values/nginx.yaml"]
+    vals = control.farm.fs["m1"]["/opt/kubeoperator/charts/values/nginx.yaml"]
+    assert b"replicas: 2" in vals and b"note: '{{ inventory_hostname }}'" in vals  # user data, never templated
     assert "/opt/kubeoperator/charts/nginx/templates/deployment.yaml" in control.farm.fs["m1"]
 
     e = deploy.create("demo", "app-deploy", {"chart": "pytorch-rocm-train", "release": "llama-8x", "namespace": "train",

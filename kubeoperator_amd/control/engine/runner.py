@@ -234,6 +234,19 @@ class HostState:
     notified: set = field(default_factory=set)
 
 
+# connection secrets stay with the transport: templates (and so anything an API user can put in a cluster
+# config or execution parameter) never see them -- the roles do not need them (they connect through the
+# engine, which reads them from the inventory directly, ``Runner._conn``)
+SECRET_VARS = ("ansible_ssh_pass", "ansible_password", "ansible_become_pass", "ansible_become_password",
+               "ansible_ssh_private_key_file")
+
+
+def _without_secrets(v: dict) -> dict:
+    for k in SECRET_VARS:
+        v.pop(k, None)
+    return v
+
+
 class _HostVars(dict):
     def __init__(self, runner: "Runner"):
         super().__init__()
@@ -241,7 +254,7 @@ class _HostVars(dict):
 
     def __getitem__(self, host):
         # inventory + facts + extra vars (as Ansible's HostVars); templated values render on lookup
-        return LazyVars({**self._r.base_vars(host), **self._r.extra_vars})
+        return LazyVars(_without_secrets({**self._r.base_vars(host), **self._r.extra_vars}))
 
     def __contains__(self, host):
         return host in self._r.inventory.hosts
@@ -284,7 +297,7 @@ class Runner:
     def task_vars(self, host: str, task: dict, item=None, loop_var="item") -> dict:
         v = {}
         v.update(task.get("_role_defaults", {}))
-        v.update(self.base_vars(host))
+        v.update(_without_secrets(self.base_vars(host)))
         v.update(self._play_vars)
         v.update(task.get("_role_vars", {}))
         v.update(task.get("vars", {}) or {})

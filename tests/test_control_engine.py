@@ -241,6 +241,22 @@ def test_templates_are_sandboxed_and_recursion_bounded():
         render("{{ a }}", v)
 
 
+def test_connection_secrets_are_not_template_visible(tmp_path):
+    """Host passwords / keys reach the transport but never the templating namespace (so a cluster config
+    such as ``x: "{{ hostvars['w1'].ansible_ssh_pass }}"`` cannot read them)."""
+    inv = _inv()
+    inv.hosts["w1"].vars["ansible_ssh_pass"] = "hunter2"
+    res, t, r = _play(tmp_path, """
+    - hosts: gpu_nodes
+      gather_facts: false
+      tasks:
+        - shell: "echo {{ ansible_ssh_pass | default('hidden') }} {{ hostvars['w1']['ansible_ssh_pass'] | default('hidden') }}"
+    """, inv=inv)
+    assert res["summary"]["success"], res["summary"]
+    assert "echo hidden hidden" in t.commands("w1")
+    assert r._conn("w1", {}).password == "hunter2"
+
+
 def test_adhoc():
     t = FakeTransport()
     t.add_rule(r"uptime", stdout="up 1 day")

@@ -861,7 +861,7 @@ def create_app() -> FastAPI:
         return [t.to_dict() for t in _all(M.CloudProviderTemplate)]
 
     crud(r, "/regions/", M.Region)
-    crud(r, "/zones/", M.Zone, on_delete=_zone_in_use)
+    crud(r, "/zones/", M.Zone, on_delete=_zone_in_use, on_create=lambda rid, data, u: cloud.on_zone_create(rid))
     crud(r, "/plans/", M.Plan, rtype="PLAN")
 
     @r.post("/cloud/region/")
@@ -878,13 +878,13 @@ def create_app() -> FastAPI:
     def cloud_zones(region: str, request: Request):
         current_user(request)
         reg = _row(M.Region, region)
-        return cloud.list_zones_from_cloud(dict(reg.vars or {}, provider=_provider_of(reg)))
+        return cloud.list_zones_from_cloud(dict(reg.vars or {}, provider=_provider_of(reg)), reg.cloud_region)
 
     @r.get("/cloud/{region}/flavor/")
     def cloud_flavors(region: str, request: Request):
         current_user(request)
         reg = _row(M.Region, region)
-        return cloud.list_flavors(dict(reg.vars or {}, provider=_provider_of(reg)))
+        return cloud.list_flavors(dict(reg.vars or {}, provider=_provider_of(reg)), reg.cloud_region)
 
     # ------------------------------------------------------------------ storage (storage/api.py)
     @r.get("/storage/nfs/")

@@ -25,11 +25,20 @@ import yaml
 from sqlalchemy import select
 
 from ..conf import RESOURCE_DIR, get_config
+from ..runtime import jobs
 from ..store import models as M
 from ..store.db import session_scope
 from . import clusters
 
 _ip_lock = threading.Lock()
+
+
+def _provider_meta(provider: str) -> dict:
+    path = os.path.join(RESOURCE_DIR, "clouds", provider, "meta.yml")
+    if not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        return yaml.safe_load(f) or {}
 
 
 def compute_models() -> list[dict]:
@@ -325,14 +334,95 @@ def destroy_resources(cluster_name: str, logger=None) -> None:
 
 # ------------------------------------------------------------------------------------------- cloud API
 def list_regions_from_cloud(provider_vars: dict) -> list[str]:
-    """Regions visible with the given credentials (reference cloud/region/); offline: configured ones."""
+    """Regions visible with the given credentials (reference cloud/region/): OpenStack Keystone regions or
+    vSphere datacenters through their REST APIs (``cloud_clients``); offline plans: the configured ones."""
+    from . import cloud_clients as cc
+
+    prov = provider_vars.get("provider", "")
+    if cc.has_endpoint(prov, provider_vars):
+        return cc.client_for(prov, provider_vars).list_regions()
     return list(provider_vars.get("regions") or ([provider_vars["region"]] if provider_vars.get("region") else []))
 
 
-def list_zones_from_cloud(region_vars: dict) -> list[str]:
+def list_zones_from_cloud(region_vars: dict, cloud_region: str | None = None) -> list:
+    """Zones of a region: OpenStack availability zones / vSphere compute clusters with their networks,
+    storages and security groups or resource pools (reference cloud/<region>/zone/)."""
+    from . import cloud_clients as cc
+
+    prov = region_vars.get("provider", "")
+    if cc.has_endpoint(prov, region_vars):
+        cli = cc.client_for(prov, region_vars, cloud_region)
+        return cli.list_zones() if prov == "openstack" else cli.list_zones(cloud_region or region_vars["datacenter"])
     return list(region_vars.get("zones") or region_vars.get("clusters") or [])
 
 
-def list_flavors(region_vars: dict) -> list[dict]:
-    """Compute flavors >= 4C/8G/60G (reference openstack client get_flavors)."""
+def list_flavors(region_vars: dict, cloud_region: str | None = None) -> list[dict]:
+    """Compute flavors >= 4C/8G/60G (reference openstack client get_flavors); vSphere and offline plans use the
+    built-in compute models."""
+    from . import cloud_clients as cc
+
+    if region_vars.get("provider") == "openstack" and cc.has_endpoint("openstack", region_vars):
+        return cc.client_for("openstack", region_vars, cloud_region).get_flavors()
     return [m for m in compute_models() if m["meta"]["cpu"] >= 4 and m["meta"]["memory"] >= 8]
+
+
+def create_image(region_vars: dict, zone_vars: dict, cloud_region: str | None = None) -> str:
+    """Import the node OS image for a zone (reference ``CloudClient.create_image``): Glance upload or a
+    vSphere content-library OVA item. Returns the image / library item id."""
+    from . import cloud_clients as cc
+
+    prov = region_vars.get("provider", "")
+    meta = _provider_meta(prov).get("image", {})
+    name = region_vars.get("image_name") or meta.get("name")
+    path = region_vars.get("image_path") or meta.get("path")
+    if prov == "openstack":
+        return cc.client_for(prov, region_vars, cloud_region).create_image(name, path)
+    if prov == "vsphere":
+        return cc.VSphereClient(region_vars).create_image(name, path, zone_vars.get("datastore") or
+                                                         region_vars.get("datastore"))
+    raise cc.CloudError(f"provider {prov!r} has no image import")
+
+
+# ------------------------------------------------------------------------------------- zone image import
+def on_zone_create(zone_id: str, run: str = "queue") -> None:
+    """Reference ``Zone.on_zone_create``: upload the node OS image for the zone in the background (Glance /
+    vSphere content library); the zone is INITIALIZING meanwhile, then READY or ERROR. Offline providers
+    (no API endpoint configured) are READY at once."""
+    from . import cloud_clients as cc
+
+    with session_scope() as s:
+        z = s.get(M.Zone, zone_id)
+        r = s.get(M.Region, z.region_id)
+        prov = zone_provider(s, z)
+        online = r is not None and cc.has_endpoint(prov, dict(r.vars or {}))
+        z.status = "INITIALIZING" if online else "READY"
+    if online:
+        if run == "queue":
+            jobs.submit("zone_create_image", {"zone_id": zone_id})
+        else:
+            jobs.run_inline("zone_create_image", {"zone_id": zone_id})
+
+
+def init_zone_image(zone_id: str, logger=None) -> dict:
+    with session_scope() as s:
+        z = s.get(M.Zone, zone_id)
+        r = s.get(M.Region, z.region_id)
+        rvars = dict(r.vars or {}, provider=zone_provider(s, z))
+        zvars, cloud_region = dict(z.vars or {}), r.cloud_region
+    try:
+        image = create_image(rvars, zvars, cloud_region)
+        status, out = "READY", {"image_id": image}
+    except Exception as e:  # noqa: BLE001 -- recorded on the zone
+        if logger:
+            logger(f"image import failed: {type(e).__name__}: {e}")
+        status, out = "ERROR", {"error": f"{type(e).__name__}: {e}"}
+    with session_scope() as s:
+        z = s.get(M.Zone, zone_id)
+        z.status = status
+        z.vars = {**(z.vars or {}), **({"image_id": out["image_id"]} if "image_id" in out else {})}
+    return dict(out, status=status)
+
+
+@jobs.task("zone_create_image")
+def _job_zone_create_image(job_id, logger, zone_id):
+    return init_zone_image(zone_id, logger=logger)

@@ -329,3 +329,149 @@ def test_monitoring_content_matches_exported_metrics():
     for rule in mon["rules"]:
         re.compile(rule["pattern"])
     assert re.search(mon["rules"][0]["pattern"], "[drm:amdgpu_job_timedout [amdgpu]] *ERROR* ring gfx_0.0.0 timeout")
+
+
+# ------------------------------------------------------------------------------------------- cloud APIs
+class _CloudStub(http.server.BaseHTTPRequestHandler):
+    """Just enough of Keystone v3 / Nova / Neutron / Cinder / Glance v2 and the vCenter REST API."""
+    uploads: dict = {}
+
+    def _send(self, code, body=None, headers=None):
+        data = json.dumps(body).encode() if body is not None else b""
+        self.send_response(code)
+        for k, v in (headers or {}).items():
+            self.send_header(k, v)
+        self.send_header("Content-Type", "application/json")
+        self.send_header("Content-Length", str(len(data)))
+        self.end_headers()
+        self.wfile.write(data)
+
+    def _body(self):
+        n = int(self.headers.get("Content-Length") or 0)
+        return self.rfile.read(n) if n else b""
+
+    def do_POST(self):
+        base = f"http://127.0.0.1:{self.server.server_port}"
+        p = self.path.split("?")[0]
+        self._body()
+        if p == "/identity/v3/auth/tokens":
+            cat = [{"type": t, "endpoints": [{"interface": "public", "region": "RegionOne", "url": f"{base}/{u}"}]}
+                   for t, u in (("compute", "compute"), ("network", "network"), ("volumev3", "volume"),
+                                ("image", "image"))]
+            return self._send(201, {"token": {"catalog": cat}}, {"X-Subject-Token": "tok-1"})
+        if p == "/image/v2/images":
+            return self._send(201, {"id": "img-1", "status": "queued"})
+        if p == "/api/session":
+            return self._send(201, "sess-1")
+        if p == "/api/content/local-library":
+            return self._send(201, "lib-1")
+        if p == "/api/content/library/item":
+            return self._send(201, "item-1")
+        if p == "/api/content/library/item/update-session":
+            return self._send(201, "us-1")
+        if p == "/api/content/library/item/update-session/us-1/file":
+            return self._send(200, {"upload_endpoint": {"uri": f"{base}/upload/item-1"}})
+        if p == "/api/content/library/item/update-session/us-1":
+            return self._send(204)
+        self._send(404, {"path": p})
+
+    def do_PUT(self):
+        _CloudStub.uploads[self.path] = len(self._body())
+        self._send(204)
+
+    def do_GET(self):
+        p = self.path.split("?")[0]
+        hdr = self.headers
+        if p.startswith(("/compute", "/network", "/volume", "/image", "/identity")) and hdr.get("X-Auth-Token") != "tok-1":
+            return self._send(401, {})
+        if p.startswith("/api/") and hdr.get("vmware-api-session-id") != "sess-1":
+            return self._send(401, {})
+        table = {
+            "/identity/v3/regions": {"regions": [{"id": "RegionOne"}]},
+            "/compute/os-availability-zone": {"availabilityZoneInfo": [{"zoneName": "nova",
+                                                                        "zoneState": {"available": True}}]},
+            "/compute/flavors/detail": {"flavors": [{"id": "1", "name": "m1.small", "vcpus": 2, "ram": 4096, "disk": 40},
+                                                    {"id": "2", "name": "gpu.8x", "vcpus": 128, "ram": 2097152,
+                                                     "disk": 960}]},
+            "/network/v2.0/networks": {"networks": [{"id": "n1", "name": "private"},
+                                                    {"id": "n2", "name": "public", "router:external": True}]},
+            "/network/v2.0/subnets": {"subnets": [{"id": "s1", "network_id": "n1", "cidr": "10.0.0.0/24"}]},
+            "/network/v2.0/security-groups": {"security_groups": [{"name": "default"}]},
+            "/volume/types": {"volume_types": [{"id": "v1", "name": "ssd"}]},
+            "/image/v2/images": {"images": []},
+            "/api/vcenter/datacenter": [{"datacenter": "datacenter-1", "name": "dc1"}],
+            "/api/vcenter/network": [{"name": "VM Network"}],
+            "/api/vcenter/datastore": [{"datastore": "ds-1", "name": "ds1", "free_space": 10 ** 12, "type": "VMFS"}],
+            "/api/vcenter/cluster": [{"cluster": "domain-c1", "name": "gpu-cluster"}],
+            "/api/vcenter/resource-pool": [{"name": "Resources"}],
+            "/api/content/library": [],
+            "/api/content/library/item": [],
+        }
+        if p in table:
+            return self._send(200, table[p])
+        self._send(404, {"path": p})
+
+    def log_message(self, *a):
+        pass
+
+
+def test_openstack_and_vsphere_rest_clients(tmp_path):
+    from kubeoperator_amd.control.domain import cloud_clients as cc
+
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), _CloudStub)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    base = f"http://127.0.0.1:{srv.server_port}"
+    img = tmp_path / "node.qcow2"
+    img.write_bytes(b"Q" * 4096)
+    try:
+        os_ = cc.OpenStackClient({"auth_url": f"{base}/identity/v3", "user_name": "u", "password": "p",
+                                  "project_name": "kube"}, region="RegionOne")
+        assert os_.list_regions() == ["RegionOne"]
+        (z,) = os_.list_zones()
+        assert z["cluster"] == "nova" and [n["name"] for n in z["networkList"]] == ["private"]
+        assert [n["name"] for n in z["floatingNetworkList"]] == ["public"] and z["securityGroups"] == ["default"]
+        assert z["networkList"][0]["subnetList"][0]["cidr"] == "10.0.0.0/24" and z["storages"][0]["name"] == "ssd"
+        assert [f["name"] for f in os_.get_flavors()] == ["gpu.8x"]  # >= 4C / 8G / 60G only
+        assert os_.create_image("node", str(img)) == "img-1"
+        assert _CloudStub.uploads["/image/v2/images/img-1/file"] == 4096
+        vc = cc.VSphereClient({"vc_host": "127.0.0.1", "vc_port": srv.server_port, "vc_scheme": "http",
+                               "vc_username": "administrator", "vc_password": "pw"})
+        assert vc.list_regions() == ["dc1"]
+        (vz,) = vc.list_zones("dc1")
+        assert vz == {"cluster": "gpu-cluster", "networks": ["VM Network"], "resourcePools": ["Resources"],
+                      "storages": [{"name": "ds1", "free": 10 ** 12, "type": "VMFS"}]}
+        assert vc.create_image("node", str(img), "ds1") == "item-1"
+        assert _CloudStub.uploads["/upload/item-1"] == 4096
+        with pytest.raises(cc.CloudError):
+            cc.OpenStackClient({"auth_url": f"{base}/nope", "user_name": "u", "password": "p", "project_name": "k"})
+    finally:
+        srv.shutdown()
+
+
+def test_zone_create_imports_image_through_the_cloud_api(control, tmp_path):
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), _CloudStub)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    img = tmp_path / "node.qcow2"
+    img.write_bytes(b"Q" * 100)
+    try:
+        with session_scope() as s:
+            reg = M.Region(name="os1", cloud_region="RegionOne", vars={
+                "provider": "openstack", "auth_url": f"http://127.0.0.1:{srv.server_port}/identity/v3",
+                "user_name": "u", "password": "p", "project_name": "kube", "image_name": "node",
+                "image_path": str(img)})
+            s.add(reg)
+            s.flush()
+            z = M.Zone(name="z1", region_id=reg.id, vars={"ip_start": "10.0.0.10", "ip_end": "10.0.0.20"})
+            off = M.Zone(name="z2", region_id=reg.id)
+            s.add_all([z, off])
+            s.flush()
+            zid = z.id
+        cloud.on_zone_create(zid, run="inline")
+        with session_scope() as s:
+            z = s.get(M.Zone, zid)
+            assert z.status == "READY" and z.vars["image_id"] == "img-1"
+        assert [r["cluster"] for r in cloud.list_zones_from_cloud(
+            {"provider": "openstack", "auth_url": f"http://127.0.0.1:{srv.server_port}/identity/v3", "user_name": "u",
+             "password": "p", "project_name": "kube"}, "RegionOne")] == ["nova"]
+    finally:
+        srv.shutdown()

@@ -89,6 +89,8 @@ def authenticate(username: str, password: str) -> dict:
             raise AuthError("unable to log in with provided credentials")
     elif context.get_settings("ldap").get("AUTH_LDAP_ENABLE") in ("true", "True", True):
         u = ldap_authenticate(username, password)
+        if not u.is_active:
+            raise AuthError("unable to log in with provided credentials")
     else:
         raise AuthError("unable to log in with provided credentials")
     with session_scope() as s:
@@ -136,51 +138,92 @@ def set_password(user_id: str, original: str | None, new: str, check_original: b
 
 
 # ------------------------------------------------------------------------------------------- LDAP
-def ldap_authenticate(username: str, password: str) -> M.User:
-    """Bind as the user against AUTH_LDAP_SERVER_URI (needs the optional ``ldap3`` package)."""
-    try:
-        import ldap3  # type: ignore
-    except ImportError as e:
-        raise AuthError("LDAP is enabled but the ldap3 package is not installed") from e
+def _ldap_settings() -> dict:
     st = context.get_settings("ldap")
-    server = ldap3.Server(st["AUTH_LDAP_SERVER_URI"])
-    conn = ldap3.Connection(server, st.get("AUTH_LDAP_BIND_DN"), st.get("AUTH_LDAP_BIND_PASSWORD"), auto_bind=True)
-    flt = st.get("AUTH_LDAP_SEARCH_FILTER", "(uid=%(user)s)") % {"user": username}
-    for ou in st.get("AUTH_LDAP_SEARCH_OU", "").split("|"):
-        conn.search(ou, flt, attributes=["mail"])
-        if conn.entries:
-            dn = conn.entries[0].entry_dn
-            ldap3.Connection(server, dn, password, auto_bind=True)
-            with session_scope() as s:
-                u = s.scalar(select(M.User).where(M.User.username == username))
-                if u is None:
-                    u = M.User(username=username, source="ldap", email=str(conn.entries[0].mail or ""))
-                    s.add(u)
-                    s.flush()
-                return u
-    raise AuthError("LDAP user not found")
+    if not st.get("AUTH_LDAP_SERVER_URI"):
+        raise AuthError("LDAP server URI is not configured")
+    return st
+
+
+def _ldap_service_conn(st: dict):
+    from .ldap_client import LDAPConnection
+
+    conn = LDAPConnection(st["AUTH_LDAP_SERVER_URI"])
+    if st.get("AUTH_LDAP_BIND_DN"):
+        conn.bind(st["AUTH_LDAP_BIND_DN"], st.get("AUTH_LDAP_BIND_PASSWORD", ""))
+    return conn
+
+
+def _attr_map(st: dict) -> dict:
+    try:
+        return json.loads(st.get("AUTH_LDAP_USER_ATTR_MAP") or '{"username": "uid", "email": "mail"}')
+    except ValueError:
+        return {"username": "uid", "email": "mail"}
+
+
+def ldap_authenticate(username: str, password: str) -> M.User:
+    """Find the user's entry with the service account (AUTH_LDAP_SEARCH_OU, ``|``-separated bases, and
+    AUTH_LDAP_SEARCH_FILTER), then bind as that DN with the given password (reference
+    users/authentication/ldap.py). The user name is escaped before it goes into the filter."""
+    from .ldap_client import LDAPConnection, LDAPError, escape_filter_value
+
+    st = _ldap_settings()
+    amap = _attr_map(st)
+    flt = (st.get("AUTH_LDAP_SEARCH_FILTER") or f"({amap.get('username', 'uid')}=%(user)s)") % {
+        "user": escape_filter_value(username)}
+    try:
+        with _ldap_service_conn(st) as conn:
+            found = None
+            for base in (st.get("AUTH_LDAP_SEARCH_OU") or "").split("|"):
+                if base.strip():
+                    hits = conn.search(base.strip(), flt, attributes=[amap.get("email", "mail")], size_limit=2)
+                    if hits:
+                        found = hits[0]
+                        break
+        if found is None:
+            raise AuthError("LDAP user not found")
+        with LDAPConnection(st["AUTH_LDAP_SERVER_URI"]) as user_conn:
+            user_conn.bind(found["dn"], password)
+    except LDAPError as e:
+        raise AuthError("invalid LDAP credentials" if e.code == 49 else f"LDAP error: {e}") from e
+    except OSError as e:
+        raise AuthError(f"LDAP server unreachable: {e}") from e
+    email = (found["attrs"].get(amap.get("email", "mail")) or [""])[0]
+    with session_scope() as s:
+        u = s.scalar(select(M.User).where(M.User.username == username))
+        if u is None:
+            u = M.User(username=username, source="ldap", email=email)
+            s.add(u)
+            s.flush()
+        elif u.source != "ldap":
+            raise AuthError("a local user with this name exists")
+        uid = u.id
+    with session_scope() as s:
+        u = s.get(M.User, uid)
+        s.expunge(u)
+        return u
 
 
 def sync_ldap_users() -> int:
-    try:
-        import ldap3  # type: ignore
-    except ImportError:
-        return 0
+    """Import every person entry under the search bases as an LDAP user (reference users/sync/ldap.py)."""
     st = context.get_settings("ldap")
-    if st.get("AUTH_LDAP_ENABLE") not in ("true", "True"):
+    if str(st.get("AUTH_LDAP_ENABLE")) not in ("true", "True") or not st.get("AUTH_LDAP_SERVER_URI"):
         return 0
-    server = ldap3.Server(st["AUTH_LDAP_SERVER_URI"])
-    conn = ldap3.Connection(server, st.get("AUTH_LDAP_BIND_DN"), st.get("AUTH_LDAP_BIND_PASSWORD"), auto_bind=True)
-    attr_map = json.loads(st.get("AUTH_LDAP_USER_ATTR_MAP", '{"username": "uid", "email": "mail"}'))
+    amap = _attr_map(st)
+    uattr, eattr = amap.get("username", "uid"), amap.get("email", "mail")
     n = 0
-    for ou in st.get("AUTH_LDAP_SEARCH_OU", "").split("|"):
-        conn.search(ou, "(objectClass=person)", attributes=list(attr_map.values()))
-        for e in conn.entries:
-            name = str(getattr(e, attr_map["username"]))
-            with session_scope() as s:
-                if s.scalar(select(M.User).where(M.User.username == name)) is None:
-                    s.add(M.User(username=name, source="ldap", email=str(getattr(e, attr_map.get("email", "mail"), ""))))
-                    n += 1
+    with _ldap_service_conn(st) as conn:
+        for base in (st.get("AUTH_LDAP_SEARCH_OU") or "").split("|"):
+            if not base.strip():
+                continue
+            for e in conn.search(base.strip(), "(|(objectClass=person)(objectClass=inetOrgPerson))", [uattr, eattr]):
+                name = (e["attrs"].get(uattr) or [""])[0]
+                if not name:
+                    continue
+                with session_scope() as s:
+                    if s.scalar(select(M.User).where(M.User.username == name)) is None:
+                        s.add(M.User(username=name, source="ldap", email=(e["attrs"].get(eattr) or [""])[0]))
+                        n += 1
     return n
 
 

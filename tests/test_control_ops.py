@@ -475,3 +475,119 @@ def test_zone_create_imports_image_through_the_cloud_api(control, tmp_path):
              "password": "p", "project_name": "kube"}, "RegionOne")] == ["nova"]
     finally:
         srv.shutdown()
+
+
+# ------------------------------------------------------------------------------------------------ LDAP
+def _ldap_server(directory: dict):
+    """A tiny LDAPv3 server (simple bind + subtree search with and / or / not / equality / presence /
+    initial-substring filters) speaking BER through the client's own codec."""
+    import socket as so
+
+    from kubeoperator_amd.control.domain import ldap_client as lc
+
+    def match(f, attrs):
+        tag, val, _ = lc.decode(f)
+        kids = [bytes([t]) + lc._len(len(v)) + v for t, v in lc.children(val)] if tag in (0xA0, 0xA1, 0xA2) else []
+        if tag == 0xA0:
+            return all(match(k, attrs) for k in kids)
+        if tag == 0xA1:
+            return any(match(k, attrs) for k in kids)
+        if tag == 0xA2:
+            return not match(kids[0], attrs)
+        if tag == 0x87:
+            return val.decode().lower() in attrs
+        a, v = [x for _, x in lc.children(val)][:2]
+        vals = [x.lower() for x in attrs.get(a.decode().lower(), [])]
+        if tag == 0xA3:
+            return v.decode().lower() in vals
+        if tag == 0xA4:
+            init = [x for t, x in lc.children(v) if t == 0x80]
+            return any(x.startswith(init[0].decode().lower()) for x in vals) if init else bool(vals)
+        return False
+
+    def handle(c):
+        buf = b""
+        while True:
+            data = c.recv(65536)
+            if not data:
+                return
+            buf += data
+            while buf:
+                try:
+                    _, msg, end = lc.decode(buf)
+                except IndexError:
+                    break
+                if end > len(buf):
+                    break
+                buf = buf[end:]
+                (_, mid), (op, body) = lc.children(msg)[:2]
+                mid = lc.as_int(mid)
+                if op == 0x60:
+                    _, dn, pw = [v for _, v in lc.children(body)][:3]
+                    ok = directory.get(dn.decode(), {}).get("_pw") == pw.decode()
+                    res = lc.seq(lc.ber_int(0 if ok else 49, 0x0A), lc.ber_str(""), lc.ber_str("" if ok else "bad"), tag=0x61)
+                    c.sendall(lc.seq(lc.ber_int(mid), res))
+                elif op == 0x63:
+                    parts = lc.children(body)
+                    base = parts[0][1].decode()
+                    f = bytes([parts[6][0]]) + lc._len(len(parts[6][1])) + parts[6][1]
+                    want = [v.decode() for _, v in lc.children(parts[7][1])]
+                    for dn, ent in directory.items():
+                        attrs = {k.lower(): v for k, v in ent.items() if k != "_pw"}
+                        if dn.endswith(base) and match(f, attrs):
+                            al = [lc.seq(lc.ber_str(k), lc.seq(*[lc.ber_str(x) for x in attrs.get(k.lower(), [])],
+                                                               tag=0x31)) for k in want if k.lower() in attrs]
+                            c.sendall(lc.seq(lc.ber_int(mid), lc.seq(lc.ber_str(dn), lc.seq(*al), tag=0x64)))
+                    c.sendall(lc.seq(lc.ber_int(mid), lc.seq(lc.ber_int(0, 0x0A), lc.ber_str(""), lc.ber_str(""),
+                                                             tag=0x65)))
+                elif op == 0x42:
+                    c.close()
+                    return
+
+    srv = so.socket()
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(8)
+
+    def loop():
+        while True:
+            try:
+                c, _ = srv.accept()
+            except OSError:
+                return
+            threading.Thread(target=handle, args=(c,), daemon=True).start()
+
+    threading.Thread(target=loop, daemon=True).start()
+    return srv
+
+
+def test_ldap_login_and_sync_with_builtin_client(control):
+    """LDAP login (service bind, search with an escaped user name, user bind) and sync through the
+    control plane's own LDAPv3 client (no ldap3 on the controller image)."""
+    from kubeoperator_amd.control.domain import context, ldap_client, users
+
+    assert ldap_client.encode_filter("(uid=alice)") == bytes.fromhex("a30c04037569640405616c696365")
+    people = "ou=people,dc=ex,dc=org"
+    srv = _ldap_server({
+        "cn=admin,dc=ex,dc=org": {"_pw": "adminpw"},
+        f"uid=alice,{people}": {"_pw": "alicepw", "uid": ["alice"], "mail": ["alice@ex.org"], "objectClass": ["person"]},
+        f"uid=bob,{people}": {"_pw": "bobpw", "uid": ["bob"], "mail": ["bob@ex.org"], "objectClass": ["inetOrgPerson"]},
+    })
+    try:
+        context.set_settings({"AUTH_LDAP_ENABLE": "true", "AUTH_LDAP_SERVER_URI": f"ldap://127.0.0.1:{srv.getsockname()[1]}",
+                              "AUTH_LDAP_BIND_DN": "cn=admin,dc=ex,dc=org", "AUTH_LDAP_BIND_PASSWORD": "adminpw",
+                              "AUTH_LDAP_SEARCH_OU": f"ou=nobody,dc=ex,dc=org|{people}",
+                              "AUTH_LDAP_SEARCH_FILTER": "(&(objectClass=*)(uid=%(user)s))"}, tab="ldap")
+        tok = users.authenticate("alice", "alicepw")
+        assert tok["token"] and tok["user"]["username"] == "alice"
+        with session_scope() as s:
+            u = s.query(M.User).filter_by(username="alice").one()
+            assert u.source == "ldap" and u.email == "alice@ex.org"
+        with pytest.raises(users.AuthError):
+            users.authenticate("alice", "wrong")
+        with pytest.raises(users.AuthError):
+            users.authenticate("*)(uid=*", "x")  # escaped: matches nobody
+        assert users.sync_ldap_users() == 1  # bob (alice exists already)
+        with session_scope() as s:
+            assert s.query(M.User).filter_by(username="bob", source="ldap").count() == 1
+    finally:
+        srv.close()

@@ -63,7 +63,18 @@ def load(trainer, directory: str, info: DistInfo, step: int | None = None) -> in
     files = _files(d)
     own = os.path.join(d, f"rank_{info.rank}.pt")
     head = torch.load(files[0], map_location="cpu", weights_only=True, mmap=True)
-    same = head["world"] == info.world and head["params"].numel() == trainer.store.params.numel()
+    if "layout" in head:  # identical flat layout (world size AND bucket boundaries): plain copy
+        lay = trainer.layout()
+        same = (head["world"] == info.world and head["layout"]["offsets"] == lay["offsets"]
+                and head["layout"]["names"] == lay["names"]
+                and [tuple(p) for p in head["layout"]["pieces"]] == [tuple(p) for p in lay["pieces"]])
+        # (pieces differ per rank under ZeRO-1: compare this rank's own file then)
+        if same is False and head["world"] == info.world and os.path.exists(own):
+            mine = torch.load(own, map_location="cpu", weights_only=True, mmap=True)
+            same = (mine["layout"]["offsets"] == lay["offsets"] and mine["layout"]["names"] == lay["names"]
+                    and [tuple(p) for p in mine["layout"]["pieces"]] == [tuple(p) for p in lay["pieces"]])
+    else:
+        same = head["world"] == info.world and head["params"].numel() == trainer.store.params.numel()
     if same:
         sd = torch.load(own, map_location=info.device, weights_only=True)
         trainer.load_state_dict(sd)

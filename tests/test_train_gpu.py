@@ -163,3 +163,30 @@ def test_fp32_gradient_buffer_matches_bf16_path(model):
     assert torch.isfinite(f32.store.params.float()).all()
     prel = ((f32.store.params.float() - b16.store.params.float()).norm() / b16.store.params.float().norm()).item()
     assert prel < 1e-2, prel
+
+
+def test_checkpoint_reshard_onto_gpu(tmp_path):
+    """A checkpoint written by a CPU run with another bucket layout loads onto the GPU trainer through the
+    resharding path (memory-mapped CPU shards copied into device state) and continues training."""
+    from kubeoperator_amd.parallel.dist import DistInfo
+    from kubeoperator_amd.train import TrainConfig, Trainer, checkpoint
+
+    tc = dict(model="tiny_llama", micro_batch=2, seq_len=128, warmup_steps=1, total_steps=10, grad_clip=0.0)
+    cpu = Trainer(TrainConfig(bucket_mb=1, **tc), DistInfo())
+    g = torch.Generator().manual_seed(3)
+    ids = torch.randint(0, cpu.cfg.vocab_size, (2, 129), generator=g)
+    batch = (ids[:, :-1].contiguous(), ids[:, 1:].contiguous())
+    cpu.train_step([batch])
+    checkpoint.save(cpu, str(tmp_path), DistInfo())
+    info = DistInfo(0, 0, 1, "none", torch.device("cuda", 0))
+    gpu = Trainer(TrainConfig(bucket_mb=0, **tc), info)
+    assert gpu.layout()["pieces"] != cpu.layout()["pieces"]
+    assert checkpoint.load(gpu, str(tmp_path), info) == 1
+    for name, p in cpu.store.named_params():
+        assert torch.equal(p, gpu.store.param(name).cpu()), name
+    ma = torch.cat([cpu.opt.master[a:b] for a, b in [(x[2], x[2] + x[1] - x[0]) for x in cpu.layout()["pieces"]]])
+    mg = torch.cat([gpu.opt.master[a:b].cpu() for a, b in [(x[2], x[2] + x[1] - x[0]) for x in gpu.layout()["pieces"]]])
+    assert torch.equal(ma[ma != 0].sort().values, mg[mg != 0].sort().values)
+    loss = gpu.train_step([(batch[0].cuda(), batch[1].cuda())])
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss) and gpu.step == 2

@@ -300,7 +300,7 @@ void flash_attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Ten
 
 }  // namespace
 
-PYBIND11_MODULE(_C, m) {
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "kubeoperator_amd gfx950 (MI355X) HIP kernels";
   m.attr("ARCH") = "gfx950";
   m.def("norm_fwd", &norm_fwd);

@@ -80,7 +80,7 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
     if force or _needs(bobj, bsrc, hdr):
         py_inc = sysconfig.get_paths()["include"]
         cmd = ["g++", "-O2", "-std=c++17", "-fPIC", abi, "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
-               "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H", "-w",
+               f"-DTORCH_EXTENSION_NAME={os.environ.get('KOP_EXT_NAME', '_C')}", "-DTORCH_API_INCLUDE_EXTENSION_H", "-w",
                "-I", CSRC, "-I", os.path.join(ROCM, "include"), "-I", py_inc]
         for i in tinc:
             cmd += ["-I", i]

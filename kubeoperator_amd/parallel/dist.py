@@ -49,6 +49,9 @@ def init_distributed(device: str = "auto", timeout_s: int = 1800) -> DistInfo:
             kw["init_method"] = init
         if use_gpu and backend == "nccl":
             kw["device_id"] = dev
+            # gradient reduce-scatters overlap the backward GEMMs: a high-priority RCCL stream lets each bucket's
+            # collective start as soon as its producer finishes instead of queueing behind the compute kernels
+            os.environ.setdefault("TORCH_NCCL_HIGH_PRIORITY", "1")
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
     elif dist.is_initialized():

@@ -504,10 +504,28 @@ def create_app() -> FastAPI:
         d = await body(request)
         return deploy.create(c.name, d.get("operation", ""), d.get("params") or {}, user=u.username)
 
+    def _own_execution(name: str, eid: str, request: Request):
+        """The execution, only through the cluster it belongs to (no reading other clusters' runs by id)."""
+        c = _cluster_for(current_user(request), name)
+        with session_scope() as s:
+            e = s.get(M.Execution, eid)
+            if e is None or e.project_id != c.project_id:
+                raise HTTPError(404, f"execution {eid} not found in cluster {name}")
+        return c
+
     @r.get("/clusters/{name}/executions/{eid}/")
     def get_execution(name: str, eid: str, request: Request):
-        _cluster_for(current_user(request), name)
+        _own_execution(name, eid, request)
         return deploy.get(eid)
+
+    @r.get("/clusters/{name}/executions/{eid}/trace/")
+    def get_execution_trace(name: str, eid: str, request: Request, view: str = "chrome"):
+        """Timing spans of the execution: ``view=chrome`` (trace-event JSON for Perfetto / chrome://tracing),
+        ``summary`` (per step: slowest tasks, per-host busy time) or ``spans``."""
+        _own_execution(name, eid, request)
+        if view not in ("chrome", "summary", "spans"):
+            raise HTTPError(400, "view must be chrome, summary or spans")
+        return deploy.get_trace(eid, view)
 
     @r.get("/clusters/{name}/apps/")
     def list_cluster_apps(name: str, request: Request):

@@ -492,6 +492,9 @@ class Local:
         from .runtime import jobs
         return jobs.tail(jobs.log_path(eid), 0, 1 << 24)[0]
 
+    def trace(self, name, eid, view):
+        return self.deploy.get_trace(eid, view)
+
     def list_packages(self):
         return self.packages.sync_packages()
 
@@ -565,6 +568,9 @@ class Remote:
     def exec_log(self, eid):
         return self._j(self.http.get(f"/tasks/{eid}/log/"))["data"]
 
+    def trace(self, name, eid, view):
+        return self._j(self.http.get(f"/clusters/{name}/executions/{eid}/trace/", params={"view": view}))
+
     def list_packages(self):
         return self._j(self.http.get("/packages/"))
 
@@ -615,6 +621,8 @@ def cmd_cluster(a, cfg) -> int:
         b.delete(a.name)
         print(f"cluster {a.name} deleted")
         return 0
+    if a.action == "trace":
+        return _trace(b, a)
     params = {}
     op = a.action
     if op == "install" and a.resume:
@@ -632,6 +640,32 @@ def cmd_cluster(a, cfg) -> int:
     elif op == "restore":
         params["clusterBackupId"] = a.backup
     return _finish(b.operate(a.name, op, params))
+
+
+def _trace(b, a) -> int:
+    """Where an execution's time went (default: the cluster's latest): per step the slowest tasks; ``-o`` writes
+    the Chrome trace-event JSON (Perfetto / chrome://tracing)."""
+    eid = a.execution
+    if not eid:
+        ex = b.executions(a.name)
+        if not ex:
+            print(f"cluster {a.name} has no executions", file=sys.stderr)
+            return 1
+        eid = ex[0]["id"]
+    if a.output:
+        with open(a.output, "w") as f:
+            json.dump(b.trace(a.name, eid, "chrome"), f)
+        print(f"trace of {eid} written to {a.output}")
+        return 0
+    sm = b.trace(a.name, eid, "summary")
+    print(f"execution {eid}: {sm['total_seconds']:.1f}s")
+    for st in sm["steps"]:
+        busy = ", ".join(f"{h} {t:.1f}s" for h, t in sorted(st["hosts"].items()))
+        print(f"\n{st['step']}: {st['seconds']:.1f}s, {st['task_count']} tasks ({st['status']}); host busy: {busy}")
+        _table([{"task": t["task"][:70], "seconds": f"{t['seconds']:.2f}", "hosts": t["hosts"],
+                 "slowest": f"{t['slowest_host']} {t['slowest_host_seconds']:.2f}s" if t["slowest_host"] else ""}
+                for t in st["tasks"]], ["task", "seconds", "hosts", "slowest"])
+    return 0
 
 
 def _set_values(pairs) -> dict:
@@ -727,7 +761,7 @@ def main(argv=None) -> int:
     c = sub.add_parser("cluster")
     c.add_argument("action", choices=["create", "list", "show", "kubeconfig", "delete", "install", "uninstall",
                                       "scale", "add-worker", "remove-worker", "upgrade", "backup", "restore",
-                                      "gpu-validate", "bigip-config"])
+                                      "gpu-validate", "bigip-config", "trace"])
     c.add_argument("name", nargs="?")
     c.add_argument("-f", "--file")
     c.add_argument("--install", action="store_true", help="with create: install right away")
@@ -738,6 +772,8 @@ def main(argv=None) -> int:
     c.add_argument("--package")
     c.add_argument("--storage")
     c.add_argument("--backup")
+    c.add_argument("--execution", help="with trace: execution id (default: the latest)")
+    c.add_argument("-o", "--output", help="with trace: write the Chrome trace-event JSON here")
     h = sub.add_parser("host")
     h.add_argument("action", choices=["add", "list", "import"])
     h.add_argument("name", nargs="?")

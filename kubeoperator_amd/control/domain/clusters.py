@@ -311,7 +311,8 @@ def extra_vars(c: M.Cluster) -> dict:
     return ev
 
 
-def run_playbook(c: M.Cluster, playbook: str, variables: dict, logger=None, forks: int | None = None) -> dict:
+def run_playbook(c: M.Cluster, playbook: str, variables: dict, logger=None, forks: int | None = None,
+                 tracer=None) -> dict:
     from ..conf import get_config
 
     path = os.path.join(plan.PLAYBOOK_DIR, plan.playbook_alias(playbook))
@@ -319,7 +320,7 @@ def run_playbook(c: M.Cluster, playbook: str, variables: dict, logger=None, fork
     cb = ResultCallback(display=logger)
     runner = Runner(inv, context.transport(), forks=forks or int(get_config()["ANSIBLE_FORKS"]), extra_vars=variables,
                     callback=cb, roles_path=[os.path.join(plan.PLAYBOOK_DIR, "roles")],
-                    controller_dir=os.path.join(get_config().data_dir, "fetch", c.name))
+                    controller_dir=os.path.join(get_config().data_dir, "fetch", c.name), tracer=tracer)
     t0 = M.now()
     res = runner.run_playbook(path)
     with session_scope() as s:

@@ -16,17 +16,22 @@ websocket); first failing playbook stops the run; a message is sent to the messa
 
 Added by design: one active execution per cluster (409 Conflict instead of silently marking the previous
 one FAILURE), ``params.resume`` re-runs an install from its first unfinished step (kubeasz tasks are
-idempotent), and ``timedelta`` is recorded in float seconds -- the cluster-create metric.
+idempotent), and ``timedelta`` is recorded in float seconds -- the cluster-create metric. Every execution
+also leaves a span trace (step -> playbook -> play -> task -> host, ``engine/trace.py``) under
+``DATA_DIR/traces``: where the minutes of a cluster-create went.
 """
 from __future__ import annotations
 
 import json
 import logging
+import os
 import re
 import time
 
 from sqlalchemy import select
 
+from ..engine.trace import Tracer, chrome_trace
+from ..engine.trace import summary as trace_summary
 from ..runtime import jobs, metrics
 from ..store import models as M
 from ..store.db import session_scope
@@ -122,6 +127,8 @@ class _Exec:
         with session_scope() as s:
             c = s.scalar(select(M.Cluster).where(M.Cluster.project_id == self.project_id))
             self.cluster_name = c.name
+        self.tracer = Tracer(on_host_span=_observe_host_span)
+        self._step_spans: dict[str, int] = {}
 
     @property
     def cluster(self) -> M.Cluster:
@@ -146,10 +153,14 @@ class _Exec:
                 st["status"] = status
                 if status == "running":
                     st["start"] = now
+                    self._step_spans[name] = self.tracer.begin(name, "step", playbook=st.get("playbook"))
                 elif status in ("success", "error") and "start" in st:
                     st["end"] = now
                     st["seconds"] = round(now - st["start"], 3)
                     metrics.STEP_SECONDS.labels(self.operation, name, status).observe(st["seconds"])
+                    sid = self._step_spans.pop(name, None)
+                    if sid is not None:
+                        self.tracer.end(sid, status)
                 self.save(current_step=i)
 
     def run_playbooks(self, ev: dict) -> dict:
@@ -164,7 +175,7 @@ class _Exec:
                 continue
             self.update_step(st["name"], "running")
             self.log(f"===== step {st['name']}: playbook {plan.playbook_alias(pb)} =====")
-            r = clusters.run_playbook(self.cluster, pb, ev, logger=self.log)
+            r = clusters.run_playbook(self.cluster, pb, ev, logger=self.log, tracer=self.tracer)
             result["summary"].update(r["summary"])
             result["raw"] = r["raw"]
             if not r["summary"].get("success", False):
@@ -209,8 +220,50 @@ def start(execution_id: str, logger=None) -> dict:
             result_summary=clusters._jsonable(result.get("summary", {})),
             result_raw=clusters._jsonable({k: v for k, v in (result.get("raw") or {}).items() if k != "ok"}))
     metrics.EXECUTION_SECONDS.labels(op, "SUCCESS" if ok else "FAILURE").observe((t1 - t0).total_seconds())
+    for name, sid in list(ex._step_spans.items()):  # steps an exception left running
+        ex.tracer.end(sid, "error")
+    _save_trace(execution_id, ex.tracer)
     _notify(c, op, ok)
     return {"success": ok, "timedelta": (t1 - t0).total_seconds()}
+
+
+def _observe_host_span(sp) -> None:
+    metrics.TASK_SECONDS.labels(sp.attrs.get("module", ""), sp.status).observe(sp.seconds)
+
+
+def _trace_path(execution_id: str) -> str:
+    from ..conf import get_config
+
+    return os.path.join(get_config().data_dir, "traces", f"{execution_id}.json")
+
+
+def _save_trace(execution_id: str, tracer: Tracer) -> None:
+    """Spans of the execution (step -> playbook -> play -> task -> host) next to its log."""
+    p = _trace_path(execution_id)
+    try:
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        tmp = p + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump({"execution_id": execution_id, "spans": tracer.to_list()}, f, default=str)
+        os.replace(tmp, p)
+    except OSError:
+        log.exception("could not write the trace of execution %s", execution_id)
+
+
+def get_trace(execution_id: str, view: str = "chrome") -> dict:
+    """``chrome``: trace-event JSON (Perfetto / chrome://tracing); ``summary``: per step the slowest tasks and
+    per-host busy time; ``spans``: the raw span list."""
+    get(execution_id)  # 404 for unknown executions
+    p = _trace_path(execution_id)
+    if not os.path.exists(p):
+        raise clusters.NotFound(f"execution {execution_id} has no trace (still running or never started)")
+    with open(p) as f:
+        spans = json.load(f)["spans"]
+    if view == "spans":
+        return {"execution_id": execution_id, "spans": spans}
+    if view == "summary":
+        return {"execution_id": execution_id, **trace_summary(spans)}
+    return chrome_trace(spans, process=f"execution {execution_id}")
 
 
 def _dispatch(ex: _Exec, c: M.Cluster, ev: dict) -> dict:

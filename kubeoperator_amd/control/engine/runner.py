@@ -270,12 +270,13 @@ class Runner:
     def __init__(self, inventory: Inventory, transport: Transport, forks: int = 5, extra_vars: dict | None = None,
                  callback: ResultCallback | None = None, roles_path: list[str] | None = None,
                  check: bool = False, tags: list | None = None, skip_tags: list | None = None,
-                 controller_dir: str | None = None, default_user: str = "root"):
+                 controller_dir: str | None = None, default_user: str = "root", tracer=None):
         self.inventory = inventory
         self.transport = transport
         self.forks = max(1, forks)
         self.extra_vars = dict(extra_vars or {})
         self.cb = callback or ResultCallback()
+        self.tracer = tracer
         self.loader = Loader(roles_path or [])
         self.check = check
         self.tags = set(tags or [])
@@ -323,13 +324,22 @@ class Runner:
             become=bool(variables.get("ansible_become", False)), extra={"connection": hv.get("ansible_connection")})
 
     # ------------------------------------------------------------------------------------ playbooks
+    def _span(self, name, kind, **attrs):
+        return self.tracer.begin(name, kind, **attrs) if self.tracer is not None else None
+
+    def _span_end(self, sid, status="ok", **attrs):
+        if sid is not None:
+            self.tracer.end(sid, status, **attrs)
+
     def run_playbook(self, path: str) -> dict:
         name = os.path.basename(path)
         self.cb.on_playbook_start(name)
+        sid = self._span(name, "playbook")
         try:
             self._run_playbook_file(path)
         finally:
             self.cb.on_playbook_end(name)
+            self._span_end(sid, "ok" if self.cb.results_summary.get("success", True) else "failed")
         return self.cb.results
 
     def _run_playbook_file(self, path: str):
@@ -344,6 +354,13 @@ class Runner:
             self.run_play(play, base)
 
     def run_play(self, play: dict, base_dir: str) -> None:
+        sid = self._span(play.get("name", play.get("hosts", "all")), "play")
+        try:
+            self._run_play(play, base_dir)
+        finally:
+            self._span_end(sid)
+
+    def _run_play(self, play: dict, base_dir: str) -> None:
         pattern = render(play.get("hosts", "all"), self.extra_vars)
         hosts = [h for h in self.inventory.match(pattern) if not self.state[h].failed and not self.state[h].unreachable]
         pname = play.get("name", pattern)
@@ -545,6 +562,13 @@ class Runner:
         if t.get("_role"):
             name = f"{t['_role']} : {name}"
         self.cb.on_task_start(name)
+        tsid = self._span(name, "task", module=mod)
+        try:
+            self._run_task_on(t, hosts, mod, raw_args, name, base_dir, handlers, tsid)
+        finally:
+            self._span_end(tsid)
+
+    def _run_task_on(self, t, hosts, mod, raw_args, name, base_dir, handlers, tsid):
         if mod not in MODULES:
             for h in hosts:
                 res = {"failed": True, "msg": f"module {mod!r} is not supported by the engine"}
@@ -555,12 +579,20 @@ class Runner:
         results: dict[str, dict] = {}
 
         def one(h):
+            hsid = self.tracer.begin(name, "host", host=h, parent=tsid, module=mod) if self.tracer is not None else None
             try:
                 results[h] = self._execute_on(h, t, mod, raw_args, name, base_dir)
             except Unreachable as e:
                 results[h] = {"unreachable": True, "msg": str(e), "changed": False}
             except (TemplateError, ModuleError, PlaybookError, KeyError, ValueError, IOError) as e:
                 results[h] = {"failed": True, "msg": f"{type(e).__name__}: {e}", "changed": False}
+            finally:
+                if hsid is not None:
+                    r = results.get(h) or {}
+                    st = ("unreachable" if r.get("unreachable") else "failed" if r.get("failed") else
+                          "skipped" if r.get("skipped") else "changed" if r.get("changed") else "ok")
+                    extra = {"rc": r["rc"]} if isinstance(r.get("rc"), int) else {}
+                    self.tracer.end(hsid, st, **extra)
 
         if len(targets) == 1 or self.forks == 1:
             for h in targets:

@@ -96,9 +96,13 @@ class SimFarm(FakeTransport):
         self._seed(conn.name)
         return super().get(conn, src)
 
+    GPU_LABEL = "/etc/kubernetes/.sim-label-gpu"  # the node's kubeoperator.io/gpu=true label (reset drops it)
+
     def _n_gpu_nodes(self) -> int:
-        """GPU hosts that are currently cluster members (joined and not reset)."""
-        return sum(1 for h, fs in self.fs.items() if self.is_gpu(h) and "/etc/kubernetes/kubelet.conf" in fs)
+        """Nodes that ``kubectl get nodes -l kubeoperator.io/gpu=true`` lists with GPUs: GPU machines that joined,
+        were labelled by the kube-node role and were not reset since."""
+        return sum(1 for h, fs in self.fs.items()
+                   if self.is_gpu(h) and "/etc/kubernetes/kubelet.conf" in fs and self.GPU_LABEL in fs)
 
     def _install_rules(self):
         R = self.add_rule
@@ -125,6 +129,12 @@ class SimFarm(FakeTransport):
                 if p.startswith("/etc/kubernetes/"):
                     del fs[p]
             return 0, "", ""
+
+        def label_gpu(host, cmd, fs):
+            node = cmd.split("kubectl label node ", 1)[1].split()[0]
+            with self._lock:
+                self.fs.setdefault(node, {})[self.GPU_LABEL] = b"true"
+            return 0, f"node/{node} labeled", ""
 
         def cat_conf(host, cmd, fs):
             data = fs.get("/etc/kubernetes/admin.conf")
@@ -173,6 +183,7 @@ class SimFarm(FakeTransport):
         R(r"kubectl -n kube-system logs", stdout="Marketing Name: AMD Instinct MI355X\n  Name: gfx950")
         R(r"lspci -nn -d 1002:", fn=gpu_probe)
         R(r"cat /etc/kubernetes/admin.conf", fn=cat_conf)
+        R(r"kubectl label node \S+ .*kubeoperator\.io/gpu=true", fn=label_gpu)
         R(r"date \+%s", fn=lambda h, c, fs: (0, str(int(time.time())), ""))
         R(r"create token kubeoperator-admin", stdout="sim-sa-token")
         R(r"zip -qr cluster-backup.zip", fn=snapshot_zip)

@@ -14,6 +14,9 @@ EXECUTION_SECONDS = Histogram("kubeoperator_execution_seconds", "Wall time of cl
 STEP_SECONDS = Histogram("kubeoperator_step_seconds", "Wall time of execution steps (playbooks)",
                          ["operation", "step", "status"], buckets=_DURATION_BUCKETS, registry=REGISTRY)
 JOBS_TOTAL = Counter("kubeoperator_jobs_total", "Background jobs finished", ["name", "state"], registry=REGISTRY)
+TASK_SECONDS = Histogram("kubeoperator_task_seconds", "Wall time of one playbook task on one host",
+                         ["module", "status"], buckets=(0.05, 0.1, 0.25, 0.5, 1, 2.5, 5, 10, 30, 60, 120, 300, 600,
+                                                        float("inf")), registry=REGISTRY)
 TASKS_TOTAL = Counter("kubeoperator_playbook_tasks_total", "Playbook task results per host",
                       ["status"], registry=REGISTRY)
 

@@ -272,8 +272,8 @@ views.cluster = async (v, [name, tab = "overview", arg]) => {
     const cur = arg || (execs[0] && execs[0].id);
     t.innerHTML = `<div class="row"><div style="flex:0 0 320px">${table(execs, [["Operation", (e) => `<a href="#/cluster/${esc(name)}/deploy/${esc(e.id)}">${esc(e.operation)}</a>`],
       ["State", (e) => st(e.state)], ["Time", (e) => `${(e.timedelta || 0).toFixed(1)}s`]])}</div>
-      <div><div id="steps" class="steps"></div><pre class="term" id="term"></pre></div></div>`;
-    if (cur) follow(cur);
+      <div><div id="steps" class="steps"></div><pre class="term" id="term"></pre><div id="trace"></div></div></div>`;
+    if (cur) follow(cur, name);
   } else if (tab === "health") {
     const [h, hist, comps, nss] = await Promise.all([GET(`/cluster/${name}/health/all/`).catch((e) => ({error: e.message})), GET(`/clusterHealthHistory/${c.project_id}/`).catch(() => []),
       GET(`/cluster/${name}/component/`).catch(() => []), GET(`/cluster/${name}/namespace/`).catch(() => [])]);
@@ -367,12 +367,33 @@ views.cluster = async (v, [name, tab = "overview", arg]) => {
   }
 };
 
-function follow(eid) {
+// Where an execution's time went: per step, its slowest tasks (span trace summary), and the full trace as
+// Chrome trace-event JSON for Perfetto / chrome://tracing.
+async function showTrace(name, eid) {
+  const box = $("#trace");
+  if (!box || box.dataset.eid === eid) return;
+  box.dataset.eid = eid;
+  const sm = await GET(`/clusters/${name}/executions/${eid}/trace/?view=summary`).catch(() => null);
+  if (!sm) { box.innerHTML = ""; return; }
+  box.innerHTML = `<h3>Time breakdown (${sm.total_seconds.toFixed(1)} s) <button class="link" id="dltrace">download trace</button></h3>` +
+    sm.steps.map((s) => `<h4>${esc(s.step)} — ${s.seconds.toFixed(1)} s, ${s.task_count} tasks ${st(s.status)}</h4>` +
+      table(s.tasks, [["Slowest tasks", "task"], ["Seconds", (x) => x.seconds.toFixed(2)], ["Hosts", "hosts"],
+        ["Slowest host", (x) => x.slowest_host ? `${esc(x.slowest_host)} (${x.slowest_host_seconds.toFixed(2)} s)` : ""]])).join("");
+  $("#dltrace").onclick = async () => {
+    const tr = await GET(`/clusters/${name}/executions/${eid}/trace/`);
+    const a = document.createElement("a");
+    a.href = URL.createObjectURL(new Blob([JSON.stringify(tr)], {type: "application/json"}));
+    a.download = `execution-${eid}.trace.json`; a.click(); URL.revokeObjectURL(a.href);
+  };
+}
+
+function follow(eid, name) {
   closeSockets();
   const term = $("#term"), steps = $("#steps");
   const tok = localStorage.getItem("kop_token");
   const p = new WebSocket(wsURL(`/ws/progress/${eid}/?token=${encodeURIComponent(tok)}`));
-  p.onmessage = (m) => { const d = JSON.parse(m.data); steps.innerHTML = (d.steps || []).map((s) => `<span class="${esc(s.status)}">${esc(s.name)}</span>`).join("") + ` ${st(d.state)}`; };
+  p.onmessage = (m) => { const d = JSON.parse(m.data); steps.innerHTML = (d.steps || []).map((s) => `<span class="${esc(s.status)}">${esc(s.name)}</span>`).join("") + ` ${st(d.state)}`;
+    if (name && (d.state === "SUCCESS" || d.state === "FAILURE")) showTrace(name, eid); };
   const l = new WebSocket(wsURL(`/ws/tasks/${eid}/log/?token=${encodeURIComponent(tok)}`));
   l.onmessage = (m) => { term.textContent += JSON.parse(m.data).message.replace(/\r\n/g, "\n"); term.scrollTop = term.scrollHeight; };
   liveSockets.push(p, l);

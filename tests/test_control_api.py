@@ -86,6 +86,25 @@ def test_cluster_lifecycle_over_http_and_ws(client):
     execs = client.get("/api/v1/clusters/demo/executions/").json()
     assert execs[0]["operation"] == "install"
 
+    # span trace of the install: steps -> playbooks -> plays -> tasks -> per-host module runs
+    tr = client.get(f"/api/v1/clusters/demo/executions/{eid}/trace/").json()
+    evs = [e for e in tr["traceEvents"] if e["ph"] == "X"]
+    cats = {e["cat"] for e in evs}
+    assert {"step", "playbook", "play", "task", "host"} <= cats
+    tracks = {e["args"]["name"] for e in tr["traceEvents"] if e["ph"] == "M" and e["name"] == "thread_name"}
+    assert {"controller", "m1", "w1"} <= tracks
+    steps = [e for e in evs if e["cat"] == "step"]
+    assert [e["name"] for e in steps] == [s["name"] for s in msg["steps"]]
+    for a, b in zip(steps, steps[1:]):  # steps run back to back, each inside the execution's wall time
+        assert b["ts"] >= a["ts"] + a["dur"] - 1
+    summ = client.get(f"/api/v1/clusters/demo/executions/{eid}/trace/", params={"view": "summary"}).json()
+    assert [s["step"] for s in summ["steps"]] == [s["name"] for s in msg["steps"]]
+    assert all(s["task_count"] > 0 and s["tasks"] and set(s["hosts"]) <= {"m1", "w1", "localhost"}
+               for s in summ["steps"])
+    assert client.get(f"/api/v1/clusters/demo/executions/{eid}/trace/", params={"view": "x"}).status_code == 400
+    assert client.get("/api/v1/clusters/demo/executions/nope/trace/").status_code == 404
+    assert b"kubeoperator_task_seconds_bucket" in client.get("/metrics").content
+
     # a second operation while one is queued is rejected
     client.post("/api/v1/clusters/demo/executions/", json={"operation": "gpu-validate"})
     r = client.post("/api/v1/clusters/demo/executions/", json={"operation": "gpu-validate"})

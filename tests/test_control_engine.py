@@ -155,6 +155,66 @@ def test_runner_failure_stops_host_and_unreachable(tmp_path):
     assert res["raw"]["unreachable"].get("w2")
 
 
+def test_runner_span_trace_nests_and_records_host_status(tmp_path):
+    """Execution tracing: playbook -> play -> task spans on the controller track, one host span per
+    module run under its task, with the result status; exported as Chrome trace events and a summary."""
+    from kubeoperator_amd.control.engine.trace import Tracer, chrome_trace, summary
+
+    t = FakeTransport()
+    t.add_rule(r"^boom$", rc=3, hosts=("w1",))
+    seen = []
+    tr = Tracer(on_host_span=seen.append)
+    sid = tr.begin("install", "step")
+    res, t, _ = _play(tmp_path, """
+    - name: workers
+      hosts: kube-worker
+      gather_facts: false
+      tasks:
+        - name: first
+          shell: "echo hi"
+        - name: boom
+          shell: boom
+          ignore_errors: true
+        - name: skipped on w2
+          shell: "echo gpu"
+          when: gpu is defined
+    """, transport=t, tracer=tr)
+    tr.end(sid, "success")
+    spans = tr.to_list()
+    by = {}
+    for s in spans:
+        by.setdefault(s["kind"], []).append(s)
+    assert [s["name"] for s in by["playbook"]] == ["site.yml"] and by["playbook"][0]["parent"] == sid
+    assert [s["name"] for s in by["play"]] == ["workers"] and by["play"][0]["parent"] == by["playbook"][0]["id"]
+    assert [s["name"] for s in by["task"]] == ["first", "boom", "skipped on w2"]
+    assert all(s["parent"] == by["play"][0]["id"] for s in by["task"])
+    hosts = {(s["name"], s["host"]): s for s in by["host"]}
+    assert hosts[("boom", "w1")]["status"] == "failed" and hosts[("boom", "w1")]["attrs"]["rc"] == 3
+    assert hosts[("boom", "w2")]["status"] in ("ok", "changed")
+    assert hosts[("skipped on w2", "w2")]["status"] == "skipped"
+    assert all(s["end"] is not None and s["end"] >= s["start"] for s in spans)
+    assert len(seen) == len(by["host"]) == 6
+    ct = chrome_trace(spans)
+    x = [e for e in ct["traceEvents"] if e["ph"] == "X"]
+    assert len(x) == len(spans) and {e["tid"] for e in x if e["cat"] == "host"} == {1, 2}
+    sm = summary(spans)
+    assert sm["steps"][0]["step"] == "install" and sm["steps"][0]["task_count"] == 3
+    assert set(sm["steps"][0]["hosts"]) == {"w1", "w2"}
+
+
+def test_tracer_closes_spans_an_exception_left_open():
+    from kubeoperator_amd.control.engine.trace import Tracer
+
+    tr = Tracer()
+    with pytest.raises(RuntimeError):
+        with tr.span("step", "step"):
+            tr.begin("pb", "playbook")
+            tr.begin("t", "task")
+            raise RuntimeError("x")
+    st = {s["kind"]: s["status"] for s in tr.to_list()}
+    assert st == {"step": "error", "playbook": "aborted", "task": "aborted"} and tr.current() is None
+
+
 def test_runner_delegate_run_once_serial_tags(tmp_path):
     res, t, _ = _play(tmp_path, """
     - hosts: k8s

@@ -173,9 +173,34 @@ def test_ui_script_parses_and_covers_the_reference_modules():
     for tab in ("overview", "nodes", "deploy", "apps", "health", "events", "storage", "backup", "grade", "configs",
                 "f5", "terminal"):
         assert f'tab === "{tab}"' in src or tab == "overview", tab
+    assert "/trace/?view=summary" in src  # deploy tab: time breakdown of the execution's span trace
     node = shutil.which("node")
     if node:
         r = subprocess.run([node, "--harmony-nullish", "--harmony-optional-chaining", "--check", path],
                            capture_output=True, text=True)
         if "bad option" not in r.stderr:
             assert r.returncode == 0, r.stderr
+
+
+def test_kubeopsctl_cluster_create_install_and_trace(tmp_path):
+    """kubeopsctl cluster create -f <plan> --install on the simulated farm, then ``cluster trace``: the per-step
+    time breakdown and the Chrome trace file of the install."""
+    cfgp = tmp_path / "config.yml"
+    cfgp.write_text(f"DATA_DIR: {tmp_path}/data\nDEFAULT_TRANSPORT: sim\n")
+    env = dict(os.environ, KUBEOPERATOR_CONFIG=str(cfgp), KOP_PBKDF2_ITERS="1000")
+    run = lambda *a: subprocess.run([sys.executable, "-m", "kubeoperator_amd.control.cli", *a], env=env,  # noqa: E731
+                                    capture_output=True, text=True, timeout=300)
+    plan = os.path.join(os.path.dirname(__file__), "..", "examples", "cluster-plan-mi355x.yml")
+    r = run("cluster", "create", "-f", plan, "--install")
+    assert r.returncode == 0 and "install: SUCCESS" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+    r = run("cluster", "trace", "mi355x-demo")
+    assert r.returncode == 0, r.stderr
+    for step in ("config", "prepare", "master", "worker", "addon"):
+        assert f"\n{step}: " in r.stdout, r.stdout
+    assert "cp-1" in r.stdout and "gpu-1" in r.stdout
+    out = tmp_path / "install.trace.json"
+    r = run("cluster", "trace", "mi355x-demo", "-o", str(out))
+    assert r.returncode == 0, r.stderr
+    import json as _json
+    ev = _json.loads(out.read_text())["traceEvents"]
+    assert any(e.get("cat") == "host" for e in ev) and any(e.get("cat") == "step" for e in ev)

@@ -828,8 +828,6 @@ def _split_top_level(s: str) -> list[str]:
 
 def _parse_free_form(mod: str, s: str) -> dict:
     """``shell: echo hi`` -> {_raw_params}; ``copy: src=a dest=b`` -> {src, dest}."""
-    import shlex
-
     if mod in ("shell", "command", "raw", "script", "include_vars", "meta"):
         # command modules accept trailing k=v options like chdir= / creates=
         args = {}

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import os
 import sys
 import time
 
@@ -38,7 +39,15 @@ def main(argv=None) -> int:
     ap.add_argument("--cuda-graph", type=int, default=0, choices=[0, 1],
                     help="replay micro-batches as captured HIP graphs (one GPU; small micro-batches)")
     ap.add_argument("--metrics-port", type=int, default=0, help="rank 0 serves Prometheus metrics here (0: off)")
+    ap.add_argument("--inject-fault", default="",
+                    help="fault injection 'RANK:STEP': that rank dies abruptly after finishing STEP (before its "
+                         "checkpoint) on the first attempt only (TORCHELASTIC_RESTART_COUNT 0), to exercise "
+                         "torchrun --max-restarts + --resume")
     a = ap.parse_args(argv)
+    fault = None
+    if a.inject_fault:
+        fr, _, fs = a.inject_fault.partition(":")
+        fault = (int(fr), int(fs))
 
     import torch
 
@@ -93,6 +102,10 @@ def main(argv=None) -> int:
                                     step_s=dt, tokens_per_s=toks, tflops=rec["tflops_per_gpu"],
                                     comm_bytes_delta=tr.dp.comm_bytes - comm_seen)
                     comm_seen = tr.dp.comm_bytes
+        if (fault is not None and (info.rank, tr.step) == fault
+                and os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") == "0"):
+            print(json.dumps({"event": "injected_fault", "rank": info.rank, "step": tr.step}), flush=True)
+            os._exit(17)  # no cleanup, no barrier: a crashed worker as the elastic agent sees it
         if a.ckpt_dir and a.ckpt_every and tr.step % a.ckpt_every == 0:
             checkpoint.save(tr, a.ckpt_dir, info)
     if metrics is not None:

@@ -47,6 +47,14 @@ def init_distributed(device: str = "auto", timeout_s: int = 1800) -> DistInfo:
         init = os.environ.get("KOP_DIST_INIT")  # e.g. file:///tmp/x (tests: no TCP port race)
         if init:
             kw["init_method"] = init
+        elif os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True":
+            # Under torchrun the agent hosts the store and keeps it across elastic restarts (static
+            # rendezvous), while env:// adds no per-attempt prefix: a restarted attempt would read the crashed
+            # attempt's process-group keys (gloo peer addresses / the RCCL unique id) and connect to dead ranks.
+            # One prefix per restart keeps every attempt's rendezvous keys apart.
+            store = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world, is_master=False,
+                                  timeout=datetime.timedelta(seconds=timeout_s))
+            kw["store"] = dist.PrefixStore(f"kop/attempt_{os.environ.get('TORCHELASTIC_RESTART_COUNT', '0')}", store)
         if use_gpu and backend == "nccl":
             kw["device_id"] = dev
             # gradient reduce-scatters overlap the backward GEMMs: a high-priority RCCL stream lets each bucket's

@@ -152,6 +152,8 @@ class FlatParamStore:
         self.gates: dict[int, object] = {}  # bucket index -> torch.cuda.Event | collective work
         self.use_order: list[int] = []  # bucket indices in the order the forward pass first reads them
         self._used: set[int] = set()
+        self._side = None  # weight-gradient stream (ops.functional._sink)
+        self.wgrad_stream = False  # issue weight gradients on it (set by the trainer)
         name_to_bucket = {nm: b for b in self.buckets for nm in b.names}
         for s in specs:
             n = s.param.numel()
@@ -223,7 +225,25 @@ class FlatParamStore:
             return
         b.pending -= 1
         if b.pending == 0 and self.on_ready is not None:
-            self.on_ready(b)
+            if self._side is not None:
+                # the bucket's gradients come from both streams: its collective is issued from the side stream
+                # after that stream has also caught up with everything the compute stream wrote so far
+                self._side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(self._side):
+                    self.on_ready(b)
+            else:
+                self.on_ready(b)
+
+    # weight-gradient stream ---------------------------------------------------------------------
+    def side_stream(self):
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
+
+    def join_side(self) -> None:
+        """The compute stream waits for every weight gradient issued on the side stream (end of backward)."""
+        if self._side is not None:
+            torch.cuda.current_stream().wait_stream(self._side)
 
     # forward gates ------------------------------------------------------------------------------
     def await_param(self, p) -> None:

@@ -34,6 +34,9 @@ def main(argv=None) -> int:
     ap.add_argument("--device", default="auto")
     ap.add_argument("--gemm-tuning", default="use", choices=["off", "use", "tune"])
     ap.add_argument("--overlap-opt", type=int, default=1, choices=[0, 1])
+    ap.add_argument("--wgrad-stream", default="auto", choices=["auto", "on", "off"],
+                    help="weight-gradient GEMMs on a second HIP stream beside the data-gradient chain "
+                         "(auto: models narrower than 2048, where it measured +8 %% on GPT-2-small)")
     ap.add_argument("--grad-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="gradient buffer precision (fp32: accumulation and DP reduction in fp32)")
     ap.add_argument("--cuda-graph", type=int, default=0, choices=[0, 1],
@@ -64,7 +67,8 @@ def main(argv=None) -> int:
     gemm_tuning.setup(a.gemm_tuning, rank=info.rank)
     tc = TrainConfig(model=a.model, micro_batch=a.mbs, seq_len=a.seq, grad_accum=a.accum, lr=a.lr,
                      warmup_steps=a.warmup, total_steps=a.steps, dp_mode=a.dp, bucket_mb=a.bucket_mb, overlap_optimizer=bool(a.overlap_opt),
-                     cuda_graph=bool(a.cuda_graph), grad_dtype=a.grad_dtype)
+                     cuda_graph=bool(a.cuda_graph), grad_dtype=a.grad_dtype,
+                     wgrad_stream=a.wgrad_stream)
     tr = Trainer(tc, info)
     if a.resume and a.ckpt_dir:
         s = checkpoint.load(tr, a.ckpt_dir, info)

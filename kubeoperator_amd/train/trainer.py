@@ -7,6 +7,7 @@ when logging.
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import asdict, dataclass, field
 
@@ -39,6 +40,7 @@ class TrainConfig:
     transposed_weights: bool = True  # keep W^T copies of wide weights for the dX GEMMs (GPU only)
     cuda_graph: bool = False  # replay each micro-batch's forward + backward as a captured HIP graph (1 GPU)
     grad_dtype: str = "bf16"  # bf16 | fp32: gradient buffer (micro-batch accumulation + DP reduction) precision
+    wgrad_stream: str = "auto"  # weight-gradient GEMMs on a side stream: auto (narrow models, hidden < 2048) | on | off
     seed: int = 1234
     model_overrides: dict = field(default_factory=dict)
 
@@ -75,6 +77,12 @@ class Trainer:
         if tc.transposed_weights and dev.type == "cuda":
             self.store.enable_transposed()
             self.store.refresh_transposed()
+        if tc.wgrad_stream not in ("auto", "on", "off"):
+            raise ValueError(f"wgrad_stream must be auto, on or off, not {tc.wgrad_stream!r}")
+        env = os.environ.get("KOP_WGRAD_STREAM")
+        want = (tc.wgrad_stream == "on" or (tc.wgrad_stream == "auto" and self.cfg.hidden < 2048)) \
+            if env not in ("0", "1") else env == "1"
+        self.store.wgrad_stream = dev.type == "cuda" and not tc.cuda_graph and want
         self.opt = FusedAdamW(self.dp.optimizer_segments(), lr=tc.lr, betas=tc.betas, eps=tc.eps,
                               weight_decay=tc.weight_decay, max_grad_norm=tc.grad_clip,
                               grad_scale=self.dp.grad_scale / tc.grad_accum, norm_allreduce=self.dp.norm_allreduce(),
@@ -111,6 +119,7 @@ class Trainer:
             loss = self.model(ids, tgt)
             loss.backward()
             losses.append(loss.detach())
+        self.store.join_side()
         self.dp.finish_grads()
         self.opt.step(lr_at(self.step, self.tc))
         self.dp.after_step()

@@ -12,6 +12,7 @@ import math
 
 import torch
 import torch.nn as nn
+from torch.utils.checkpoint import checkpoint
 
 from ..ops import functional as kf
 from ..parallel.flat import ParamSpec
@@ -60,6 +61,7 @@ class GPT2(nn.Module):
         self.layers = nn.ModuleList([GPT2Block(cfg) for _ in range(cfg.n_layers)])
         self.lnf_w = nn.Parameter(torch.empty(cfg.hidden))
         self.lnf_b = nn.Parameter(torch.empty(cfg.hidden))
+        self.recompute = False  # activation recompute per block (set by the trainer)
 
     def param_specs(self) -> list[ParamSpec]:
         c = self.cfg
@@ -89,6 +91,9 @@ class GPT2(nn.Module):
         x = kf.embedding(ids.reshape(-1), self.wte) + kf.embedding(pos, self.wpe)
         pending = None
         for blk in self.layers:
-            x, pending = blk(x, pending, B, S)
+            if self.recompute and torch.is_grad_enabled():
+                x, pending = checkpoint(blk, x, pending, B, S, use_reentrant=False)
+            else:
+                x, pending = blk(x, pending, B, S)
         y, _ = kf.layer_norm(x, self.lnf_w, self.lnf_b, self.cfg.norm_eps, residual=pending)
         return kf.cross_entropy_lmhead(y, self.wte, targets.reshape(-1))

@@ -40,6 +40,7 @@ class TrainConfig:
     transposed_weights: bool = True  # keep W^T copies of wide weights for the dX GEMMs (GPU only)
     cuda_graph: bool = False  # replay each micro-batch's forward + backward as a captured HIP graph (1 GPU)
     grad_dtype: str = "bf16"  # bf16 | fp32: gradient buffer (micro-batch accumulation + DP reduction) precision
+    recompute: bool = False  # per-block activation recompute (long sequences: only block inputs stay saved)
     wgrad_stream: str = "auto"  # weight-gradient GEMMs on a side stream: auto (narrow models, hidden < 2048) | on | off
     seed: int = 1234
     model_overrides: dict = field(default_factory=dict)
@@ -59,13 +60,19 @@ class Trainer:
     def __init__(self, tc: TrainConfig, info: DistInfo):
         self.tc = tc
         self.info = info
-        self.cfg = get_config(tc.model, **tc.model_overrides)
+        overrides = dict(tc.model_overrides)
+        base = get_config(tc.model)
+        if tc.seq_len > base.max_seq_len and base.arch == "llama" and "max_seq_len" not in overrides:
+            overrides["max_seq_len"] = tc.seq_len  # RoPE: the context length is a limit, not a weight shape
+        self.cfg = get_config(tc.model, **overrides)
         if tc.seq_len > self.cfg.max_seq_len:
-            raise ValueError(f"seq_len {tc.seq_len} > model max_seq_len {self.cfg.max_seq_len}")
+            raise ValueError(f"seq_len {tc.seq_len} > model max_seq_len {self.cfg.max_seq_len} "
+                             "(learned positions cannot be extended)")
         dev = info.device
         t0 = time.time()
         with torch.device("meta"):
             self.model = build_model(self.cfg)
+        self.model.recompute = bool(tc.recompute)
         if tc.grad_dtype not in ("bf16", "fp32"):
             raise ValueError(f"grad_dtype must be bf16 or fp32, not {tc.grad_dtype!r}")
         self.store = FlatParamStore(self.model, self.model.param_specs(), dev, world=info.world,

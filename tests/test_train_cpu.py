@@ -34,6 +34,29 @@ def test_loss_decreases(model):
     assert abs(losses[0] - torch.log(torch.tensor(float(tr.cfg.vocab_size)))) < 1.0  # random init ~ uniform
 
 
+@pytest.mark.parametrize("model", ["tiny_llama", "tiny_gpt2"])
+def test_activation_recompute_matches_saved_activations(model):
+    """Per-block recompute (``--recompute``) re-runs each block's forward in backward: same gradients, so the
+    same parameters after two optimizer steps, as keeping every activation."""
+    a = Trainer(_tc(model=model, grad_accum=2), DistInfo())
+    b = Trainer(_tc(model=model, grad_accum=2, recompute=True), DistInfo())
+    assert b.model.recompute and not a.model.recompute
+    for step in range(2):
+        mbs = [_batch(a, seed=10 * step + i) for i in range(2)]
+        la, lb = a.train_step(mbs), b.train_step(mbs)
+        torch.testing.assert_close(la, lb, atol=1e-6, rtol=0)
+    torch.testing.assert_close(a.store.params.float(), b.store.params.float(), atol=1e-6, rtol=0)
+    torch.testing.assert_close(a.opt.exp_avg, b.opt.exp_avg, atol=1e-7, rtol=1e-5)
+
+
+def test_llama_context_extends_past_config_limit():
+    tr = Trainer(_tc(seq_len=512, recompute=True), DistInfo())  # tiny_llama's configured limit is 256
+    assert tr.cfg.max_seq_len == 512
+    assert float(tr.train_step([_batch(tr, seq=512)])) > 0
+    with pytest.raises(ValueError, match="learned positions"):
+        Trainer(_tc(model="tiny_gpt2", seq_len=512), DistInfo())
+
+
 def test_grad_accum_equals_big_batch():
     t1 = Trainer(_tc(micro_batch=4), DistInfo())
     t2 = Trainer(_tc(micro_batch=2, grad_accum=2), DistInfo())

@@ -45,6 +45,9 @@ def main() -> int:
                     help="hipBLASLt solution selection: committed TunableOp winners (use), heuristic (off), re-tune")
     ap.add_argument("--overlap-opt", type=int, default=1, choices=[0, 1],
                     help="run AdamW on its own stream, gated per bucket into the next forward (1) or serially (0)")
+    ap.add_argument("--fp8", type=int, default=0, choices=[0, 1],
+                    help="E4M3 forward + data-gradient GEMMs of the Llama block projections (opt-in; reported "
+                         "as dtype fp8-mixed)")
     ap.add_argument("--recompute", type=int, default=0, choices=[0, 1],
                     help="per-block activation recompute: only block inputs stay saved (long sequences, e.g. "
                          "Llama-3-8B at --seq 32768 on one GPU; ~1/3 more FLOPs)")
@@ -78,7 +81,7 @@ def main() -> int:
                      overlap_optimizer=bool(args.overlap_opt),
                      transposed_weights=os.environ.get("KOP_TRANSPOSED_W", "1") != "0",
                      cuda_graph=bool(args.cuda_graph), grad_dtype=args.grad_dtype,
-                     wgrad_stream=args.wgrad_stream, recompute=bool(args.recompute))
+                     wgrad_stream=args.wgrad_stream, recompute=bool(args.recompute), fp8=bool(args.fp8))
     trainer = Trainer(tc, info)
     data = SyntheticTokens(trainer.cfg.vocab_size, args.mbs, args.seq, info.device, seed=tc.seed, rank=info.rank)
     cuda = info.device.type == "cuda"
@@ -123,7 +126,7 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "fp8-mixed (E4M3 projection GEMMs, bf16 elsewhere)" if args.fp8 else "bf16",
             "data": "synthetic (random token ids generated on device; random-init weights)",
             "config": {
                 "model": model_name,

@@ -209,6 +209,20 @@ void transpose_(const Tensor& in, const Tensor& out) {
      "transpose (rows and columns must be multiples of 8)");
 }
 
+// ------------------------------------------------------------------ fp8
+void fp8_quant_(const Tensor& x, const Tensor& out, const Tensor& scale, const Tensor& amax_ws) {
+  check_bf16(x, "x");
+  check_gpu(out, "out");
+  check_f32(scale, "scale");
+  check_gpu(amax_ws, "amax_ws");
+  TORCH_CHECK(x.is_contiguous() && out.is_contiguous(), "fp8_quant: contiguous tensors only");
+  TORCH_CHECK(out.element_size() == 1 && out.numel() == x.numel(), "fp8_quant: out must be 1-byte, x.numel()");
+  TORCH_CHECK(scale.numel() == 1 && amax_ws.nbytes() >= 4, "fp8_quant: scale / workspace size");
+  rc(kop::fp8_quantize(bp(x), x.numel(), reinterpret_cast<uint8_t*>(out.data_ptr()), scale.data_ptr<float>(),
+                       reinterpret_cast<unsigned*>(amax_ws.data_ptr()), cur_stream()),
+     "fp8_quant (x 16-byte and out 8-byte aligned)");
+}
+
 // ------------------------------------------------------------------ optimizer
 void adamw_(const Tensor& p, const Tensor& g, const Tensor& master, const Tensor& m, const Tensor& v, double lr,
             double b1, double b2, double eps, double wd, int64_t step, double gscale,
@@ -315,6 +329,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_bwd", &gelu_bwd);
   m.def("cross_entropy_fwd_", &cross_entropy_fwd_);
   m.def("transpose_", &transpose_);
+  m.def("fp8_quant_", &fp8_quant_);
   m.def("adamw_", &adamw_);
   m.def("grad_sumsq_", &grad_sumsq_);
   m.def("clip_coef_", &clip_coef_);

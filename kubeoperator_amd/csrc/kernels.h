@@ -46,6 +46,10 @@ int clip_coef(const float* sumsq, float max_norm, float* coef, float* norm_out, 
 // transpose.hip
 int transpose2d(const bf16_t* in, bf16_t* out, int64_t R, int64_t C, int64_t ldi, int64_t ldo, hipStream_t stream);
 
+// fp8.hip: per-tensor OCP E4M3 quantization (current scaling): out = rne(clamp(x / scale)), scale = amax / 448;
+// amax_ws: one 4-byte device word of scratch
+int fp8_quantize(const bf16_t* x, int64_t n, uint8_t* out, float* scale, unsigned* amax_ws, hipStream_t stream);
+
 // flash_attn.hip
 int flash_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int S, int Hq,
                    int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, float scale, bool causal,

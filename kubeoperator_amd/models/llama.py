@@ -93,6 +93,10 @@ class Llama(nn.Module):
             specs.append(ParamSpec(f"layers.{i}.attn_norm", self.layers[i].attn_norm, False, 1, "ones"))
         return specs
 
+    def fp8_param_names(self) -> list[str]:
+        """The block projections whose forward / data-gradient GEMMs may run in E4M3 (``--fp8``)."""
+        return [f"layers.{i}.{n}" for i in range(self.cfg.n_layers) for n in ("wqkv", "wo", "w_gate_up", "w_down")]
+
     def rope_tables(self, S, device):
         key = (S, str(device))
         if key not in self._rope:

@@ -131,9 +131,25 @@ def transpose_into(x: torch.Tensor, out: torch.Tensor) -> None:
 
 
 def _dx(dy2, w):
-    """dX = dY . W through the transposed copy when the flat store keeps one (K-contiguous GEMM layout)."""
+    """dX = dY . W through the transposed copy when the flat store keeps one (K-contiguous GEMM layout);
+    in E4M3 when the store keeps an FP8 copy of it (``--fp8``, ops/fp8.py)."""
+    wt8 = getattr(w, "wt8", None)
+    if wt8 is not None:
+        from . import fp8
+
+        return fp8.mm(dy2, wt8.t(), w.wt8_scale, out_dtype=dy2.dtype)
     wt = getattr(w, "wt", None)
     return torch.mm(dy2, wt.t()) if wt is not None else torch.mm(dy2, w)
+
+
+def _fwd(x2, w):
+    """Y = X . W^T (E4M3 operands when the store keeps an FP8 copy of W)."""
+    w8 = getattr(w, "w8", None)
+    if w8 is not None:
+        from . import fp8
+
+        return fp8.mm(x2, w8.t(), w.w8_scale, out_dtype=x2.dtype)
+    return torch.mm(x2, w.t())
 
 
 def _dw_into(dy2, x2, out, accumulate):
@@ -169,7 +185,7 @@ class _Linear(Function):
     @staticmethod
     def forward(ctx, x, w, b):
         x2 = x.reshape(-1, x.shape[-1])
-        y = torch.addmm(b, x2, w.t()) if b is not None else torch.mm(x2, w.t())
+        y = torch.addmm(b, x2, w.t()) if b is not None else _fwd(x2, w)
         ctx.save_for_backward(x2, w)
         ctx.has_b = b is not None
         if b is not None:
@@ -309,7 +325,7 @@ class _LinearSwiGLU(Function):
     @staticmethod
     def forward(ctx, x, w):
         x2 = x.reshape(-1, x.shape[-1])
-        gu = torch.mm(x2, w.t())
+        gu = _fwd(x2, w)
         ctx.save_for_backward(x2, w, gu)
         ctx.in_shape = x.shape
         h = _lib().swiglu_fwd(gu)
@@ -361,7 +377,7 @@ class _SwiGLUMLP(Function):
     def forward(ctx, x, w_gu, w_d):
         lib = _lib()
         x2 = x.reshape(-1, x.shape[-1])
-        gu = torch.mm(x2, w_gu.t())
+        gu = _fwd(x2, w_gu)
         T, F2 = gu.shape
         F = F2 // 2
         ht = None
@@ -369,7 +385,7 @@ class _SwiGLUMLP(Function):
             h, ht = lib.swiglu_fwd_t(gu)
         else:
             h = lib.swiglu_fwd(gu)
-        y = torch.mm(h, w_d.t())
+        y = _fwd(h, w_d)
         ctx.save_for_backward(x2, w_gu, w_d, gu, ht if ht is not None else h)
         ctx.has_ht = ht is not None
         ctx.in_shape = x.shape

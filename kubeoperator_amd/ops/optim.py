@@ -134,11 +134,12 @@ class FusedAdamW:
                     launch(k)
                     b = self.segments[k].bucket
                     gate = self.on_segment(self.segments[k]) if self.on_segment is not None else None
-                    if self.store.has_transposed:
-                        # the transposed copies follow the bucket's final values (after the ZeRO-1 gather)
+                    if self.store.has_transposed or self.store.has_fp8:
+                        # the transposed / FP8 copies follow the bucket's final values (after the ZeRO-1 gather)
                         if gate is not None:
                             gate.wait()  # optimizer stream waits for the collective
                         self.store.refresh_transposed(b)
+                        self.store.refresh_fp8(b)
                         gate = None
                     if gate is None:
                         gate = torch.cuda.Event()

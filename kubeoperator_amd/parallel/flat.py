@@ -300,6 +300,49 @@ class FlatParamStore:
                 p = self._param_by_name[name]
                 transpose_into(p.detach(), p.wt)
 
+    # FP8 weight copies (forward / data-gradient GEMMs in E4M3, ops/fp8.py) ---------------------------
+    def enable_fp8(self, names) -> int:
+        """Keep E4M3 copies of the named 2-D weights -- ``p.w8`` ([out, in]) and, where the transposed bf16
+        copy exists, ``p.wt8`` ([in, out]) -- with their dequantization scales, refreshed per bucket after
+        every update (``refresh_fp8``). 1 byte per element and orientation (~15 GB at Llama-3-8B)."""
+        from ..ops.fp8 import FP8
+
+        self.params_fp8 = torch.empty(self.numel, dtype=FP8, device=self.device)
+        self.params_t_fp8 = torch.empty(self.numel, dtype=FP8, device=self.device) if self.has_transposed else None
+        self._fp8_names: dict[int, list[str]] = {}
+        n = 0
+        for name in names:
+            p = self._param_by_name[name]
+            if p.dim() != 2:
+                continue
+            o, k = self.offsets[name], p.numel()
+            p.w8 = self.params_fp8[o:o + k].view(p.shape)
+            p.w8_scale = torch.ones((), dtype=torch.float32, device=self.device)
+            if self.params_t_fp8 is not None and getattr(p, "wt", None) is not None:
+                p.wt8 = self.params_t_fp8[o:o + k].view(p.shape[1], p.shape[0])
+                p.wt8_scale = torch.ones((), dtype=torch.float32, device=self.device)
+            self._fp8_names.setdefault(self._bucket_of[id(p)].index, []).append(name)
+            n += 1
+        return n
+
+    @property
+    def has_fp8(self) -> bool:
+        return getattr(self, "params_fp8", None) is not None
+
+    def refresh_fp8(self, bucket: int | None = None) -> None:
+        """Re-quantize one bucket's (or every) FP8 weight copy from the bf16 values, on the current stream."""
+        if not self.has_fp8:
+            return
+        from ..ops.fp8 import quantize_into
+
+        idx = self._fp8_names.keys() if bucket is None else [bucket]
+        for b in idx:
+            for name in self._fp8_names.get(b, ()):
+                p = self._param_by_name[name]
+                quantize_into(p.detach(), p.w8, p.w8_scale)
+                if getattr(p, "wt8", None) is not None:
+                    quantize_into(p.wt, p.wt8, p.wt8_scale)
+
     def zero_grads(self) -> None:
         self.grads.zero_()
 

@@ -145,4 +145,5 @@ def _reshard(trainer, head: dict, files: list[str]) -> None:
     # bf16 parameters follow the fp32 masters of this rank's segments (identical values: they were rounded
     # from the same masters), and the transposed weight copies follow the parameters
     st.refresh_transposed()
+    st.refresh_fp8()
     trainer.step = int(head["step"])

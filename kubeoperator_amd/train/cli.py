@@ -34,6 +34,9 @@ def main(argv=None) -> int:
     ap.add_argument("--device", default="auto")
     ap.add_argument("--gemm-tuning", default="use", choices=["off", "use", "tune"])
     ap.add_argument("--overlap-opt", type=int, default=1, choices=[0, 1])
+    ap.add_argument("--fp8", type=int, default=0, choices=[0, 1],
+                    help="E4M3 forward + data-gradient GEMMs of the Llama block projections (opt-in; reported "
+                         "as dtype fp8-mixed)")
     ap.add_argument("--recompute", type=int, default=0, choices=[0, 1],
                     help="per-block activation recompute: only block inputs stay saved (long sequences, e.g. "
                          "Llama-3-8B at --seq 32768 on one GPU; ~1/3 more FLOPs)")
@@ -71,7 +74,7 @@ def main(argv=None) -> int:
     tc = TrainConfig(model=a.model, micro_batch=a.mbs, seq_len=a.seq, grad_accum=a.accum, lr=a.lr,
                      warmup_steps=a.warmup, total_steps=a.steps, dp_mode=a.dp, bucket_mb=a.bucket_mb, overlap_optimizer=bool(a.overlap_opt),
                      cuda_graph=bool(a.cuda_graph), grad_dtype=a.grad_dtype,
-                     wgrad_stream=a.wgrad_stream, recompute=bool(a.recompute))
+                     wgrad_stream=a.wgrad_stream, recompute=bool(a.recompute), fp8=bool(a.fp8))
     tr = Trainer(tc, info)
     if a.resume and a.ckpt_dir:
         s = checkpoint.load(tr, a.ckpt_dir, info)

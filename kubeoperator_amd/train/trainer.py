@@ -40,6 +40,7 @@ class TrainConfig:
     transposed_weights: bool = True  # keep W^T copies of wide weights for the dX GEMMs (GPU only)
     cuda_graph: bool = False  # replay each micro-batch's forward + backward as a captured HIP graph (1 GPU)
     grad_dtype: str = "bf16"  # bf16 | fp32: gradient buffer (micro-batch accumulation + DP reduction) precision
+    fp8: bool = False  # E4M3 forward + data-gradient GEMMs of the block projections (ops/fp8.py; opt-in)
     recompute: bool = False  # per-block activation recompute (long sequences: only block inputs stay saved)
     wgrad_stream: str = "auto"  # weight-gradient GEMMs on a side stream: auto (narrow models, hidden < 2048) | on | off
     seed: int = 1234
@@ -84,6 +85,11 @@ class Trainer:
         if tc.transposed_weights and dev.type == "cuda":
             self.store.enable_transposed()
             self.store.refresh_transposed()
+        if tc.fp8:
+            if dev.type != "cuda" or self.cfg.arch != "llama":
+                raise ValueError("fp8 GEMMs need a GPU and a Llama model")
+            self.store.enable_fp8(self.model.fp8_param_names())
+            self.store.refresh_fp8()
         if tc.wgrad_stream not in ("auto", "on", "off"):
             raise ValueError(f"wgrad_stream must be auto, on or off, not {tc.wgrad_stream!r}")
         env = os.environ.get("KOP_WGRAD_STREAM")
@@ -130,8 +136,9 @@ class Trainer:
         self.dp.finish_grads()
         self.opt.step(lr_at(self.step, self.tc))
         self.dp.after_step()
-        if self.store.has_transposed and not self.opt.overlap:
+        if (self.store.has_transposed or self.store.has_fp8) and not self.opt.overlap:
             self.store.refresh_transposed()
+            self.store.refresh_fp8()
         self.step += 1
         return torch.stack(losses).mean()
 
@@ -183,4 +190,5 @@ class Trainer:
         self.store.params.copy_(sd["params"])
         self.opt.load_state_dict(sd["optimizer"])
         self.store.refresh_transposed()
+        self.store.refresh_fp8()
         self.step = int(sd["step"])

@@ -223,6 +223,28 @@ void fp8_quant_(const Tensor& x, const Tensor& out, const Tensor& scale, const T
      "fp8_quant (x 16-byte and out 8-byte aligned)");
 }
 
+void fp8_cast_scaled_(const Tensor& x, const Tensor& scale, const Tensor& out) {
+  check_bf16(x, "x");
+  check_f32(scale, "scale");
+  TORCH_CHECK(x.is_contiguous() && out.is_contiguous() && out.is_cuda(), "fp8_cast: contiguous GPU tensors");
+  TORCH_CHECK(out.element_size() == 1 && out.numel() == x.numel(), "fp8_cast: out must be 1-byte, x.numel()");
+  rc(kop::fp8_cast_scaled(bp(x), x.numel(), scale.data_ptr<float>(), reinterpret_cast<uint8_t*>(out.data_ptr()),
+                          cur_stream()),
+     "fp8_cast (numel a multiple of 8, aligned)");
+}
+void fp8_transpose_cast_(const Tensor& in, const Tensor& scale, const Tensor& out) {
+  check_bf16(in, "in");
+  check_rows(in, "in");
+  check_f32(scale, "scale");
+  TORCH_CHECK(out.is_cuda() && out.element_size() == 1 && out.dim() == 2 && out.stride(1) == 1,
+              "fp8_transpose_cast: out must be a 2-D 1-byte GPU tensor with contiguous rows");
+  TORCH_CHECK(out.size(0) == in.size(1) && out.size(1) == in.size(0), "out must be [in.cols, in.rows]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 8 == 0, "out must be 8-byte aligned");
+  rc(kop::fp8_transpose_cast(bp(in), reinterpret_cast<uint8_t*>(out.data_ptr()), in.size(0), in.size(1),
+                             in.stride(0), out.stride(0), scale.data_ptr<float>(), cur_stream()),
+     "fp8_transpose_cast (rows and columns multiples of 8)");
+}
+
 // ------------------------------------------------------------------ optimizer
 void adamw_(const Tensor& p, const Tensor& g, const Tensor& master, const Tensor& m, const Tensor& v, double lr,
             double b1, double b2, double eps, double wd, int64_t step, double gscale,
@@ -330,6 +352,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cross_entropy_fwd_", &cross_entropy_fwd_);
   m.def("transpose_", &transpose_);
   m.def("fp8_quant_", &fp8_quant_);
+  m.def("fp8_cast_scaled_", &fp8_cast_scaled_);
+  m.def("fp8_transpose_cast_", &fp8_transpose_cast_);
   m.def("adamw_", &adamw_);
   m.def("grad_sumsq_", &grad_sumsq_);
   m.def("clip_coef_", &clip_coef_);

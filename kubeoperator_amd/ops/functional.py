@@ -144,12 +144,32 @@ def _dx(dy2, w):
 
 def _fwd(x2, w):
     """Y = X . W^T (E4M3 operands when the store keeps an FP8 copy of W)."""
+    return _fwd8(x2, w)[0]
+
+
+def _fwd8(x2, w):
+    """(Y = X . W^T, X's E4M3 dequantization scale or None): the scale is kept for the E4M3 weight gradient."""
     w8 = getattr(w, "w8", None)
     if w8 is not None:
         from . import fp8
 
-        return fp8.mm(x2, w8.t(), w.w8_scale, out_dtype=x2.dtype)
-    return torch.mm(x2, w.t())
+        x8, sx = fp8.quantize(x2)
+        return fp8.mm8(x8, sx, w8.t(), w.w8_scale, out_dtype=x2.dtype), sx
+    return torch.mm(x2, w.t()), None
+
+
+def _fp8_bwd(w, sx) -> bool:
+    """E4M3 data- and weight-gradient GEMMs: W has its E4M3 transposed copy and X was quantized in forward."""
+    return sx is not None and getattr(w, "wt8", None) is not None
+
+
+def _dx8(dy2, w):
+    """dX = dY . W in E4M3 -> (dX, dY contiguous, dY's scale)."""
+    from . import fp8
+
+    dy2 = dy2.contiguous()
+    dy8, sdy = fp8.quantize(dy2)
+    return fp8.mm8(dy8, sdy, w.wt8.t(), w.wt8_scale, out_dtype=dy2.dtype), dy2, sdy
 
 
 def _dw_into(dy2, x2, out, accumulate):
@@ -185,7 +205,11 @@ class _Linear(Function):
     @staticmethod
     def forward(ctx, x, w, b):
         x2 = x.reshape(-1, x.shape[-1])
-        y = torch.addmm(b, x2, w.t()) if b is not None else _fwd(x2, w)
+        ctx.sx = None
+        if b is not None:
+            y = torch.addmm(b, x2, w.t())
+        else:
+            y, ctx.sx = _fwd8(x2, w)
         ctx.save_for_backward(x2, w)
         ctx.has_b = b is not None
         if b is not None:
@@ -197,6 +221,16 @@ class _Linear(Function):
     def backward(ctx, dy):
         x2, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, w.shape[0])
+        if _fp8_bwd(w, ctx.sx):
+            from . import fp8
+
+            dx, dy2, sdy = _dx8(dy2, w)
+            dx = dx.view(ctx.in_shape)
+            sx = ctx.sx
+            dw = _sink(w, lambda out, acc: fp8.wgrad_into(fp8.transpose_cast(dy2, sdy), sdy,
+                                                          fp8.transpose_cast(x2, sx), sx, out, acc),
+                       dy2, x2, sdy, sx) if ctx.needs_input_grad[1] else None
+            return dx, dw, None
         dx = _dx(dy2, w).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
         dw = _sink(w, lambda out, acc: _dw_into(dy2, x2, out, acc), dy2, x2) if ctx.needs_input_grad[1] else None
         db = None
@@ -377,7 +411,7 @@ class _SwiGLUMLP(Function):
     def forward(ctx, x, w_gu, w_d):
         lib = _lib()
         x2 = x.reshape(-1, x.shape[-1])
-        gu = _fwd(x2, w_gu)
+        gu, ctx.sx = _fwd8(x2, w_gu)
         T, F2 = gu.shape
         F = F2 // 2
         ht = None
@@ -385,7 +419,7 @@ class _SwiGLUMLP(Function):
             h, ht = lib.swiglu_fwd_t(gu)
         else:
             h = lib.swiglu_fwd(gu)
-        y = _fwd(h, w_d)
+        y, ctx.sh = _fwd8(h, w_d)
         ctx.save_for_backward(x2, w_gu, w_d, gu, ht if ht is not None else h)
         ctx.has_ht = ht is not None
         ctx.in_shape = x.shape
@@ -397,6 +431,8 @@ class _SwiGLUMLP(Function):
         x2, w_gu, w_d, gu, h_or_ht = ctx.saved_tensors
         T, F2 = gu.shape
         dy2 = dy.reshape(-1, w_d.shape[0])
+        if ctx.has_ht and _fp8_bwd(w_d, ctx.sh) and _fp8_bwd(w_gu, ctx.sx):
+            return _SwiGLUMLP._backward_fp8(ctx, lib, x2, w_gu, w_d, gu, h_or_ht, dy2)
         dh = _dx(dy2, w_d)
         dw_d = None
         if ctx.needs_input_grad[2]:
@@ -418,6 +454,31 @@ class _SwiGLUMLP(Function):
             else:
                 dw_gu = _sink(w_gu, lambda out, acc: _dw_into(dgu, x2, out, acc), dgu, x2)
         return dx, dw_gu, dw_d
+
+
+    @staticmethod
+    def _backward_fp8(ctx, lib, x2, w_gu, w_d, gu, ht, dy2):
+        """All four backward GEMMs in E4M3: the data gradients quantize dY / dgu (current scaling), the weight
+        gradients reuse those scales for dY^T (transpose-cast) and dgu^T (one-pass cast of the SwiGLU kernel's
+        transposed output), and the forward's scales for h^T and X^T."""
+        from . import fp8
+
+        dh, dy2, sdy = _dx8(dy2, w_d)
+        dw_d = None
+        if ctx.needs_input_grad[2]:
+            sh = ctx.sh
+            dw_d = _sink(w_d, lambda out, acc: fp8.wgrad_into(fp8.transpose_cast(dy2, sdy), sdy,
+                                                              fp8.cast_scaled(ht, sh), sh, out, acc),
+                         dy2, ht, sdy, sh)
+        dgu, dgut = lib.swiglu_bwd_t(gu, dh.contiguous())
+        dx, dgu, sdgu = _dx8(dgu, w_gu)
+        dw_gu = None
+        if ctx.needs_input_grad[1]:
+            sx = ctx.sx
+            dw_gu = _sink(w_gu, lambda out, acc: fp8.wgrad_into(fp8.cast_scaled(dgut, sdgu), sdgu,
+                                                                fp8.transpose_cast(x2, sx), sx, out, acc),
+                          dgut, x2, sdgu, sx)
+        return dx.view(ctx.in_shape) if ctx.needs_input_grad[0] else None, dw_gu, dw_d
 
 
 def swiglu_mlp(x, w_gu, w_d):

@@ -67,3 +67,62 @@ def test_fp8_training_follows_bf16():
     b, f = curves[False], curves[True]
     assert f[-1] < f[0] - 1.0, f  # it learns
     assert abs(f[-1] - b[-1]) < 0.25 * (b[0] - b[-1]), (b[-1], f[-1])
+
+
+def _fp8_copies(w):
+    from kubeoperator_amd.ops import fp8
+
+    w.w8, w.w8_scale = fp8.quantize(w.detach())
+    w.wt = w.detach().t().contiguous()
+    w.wt8, w.wt8_scale = fp8.quantize(w.wt)
+    return w
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+
+def test_fp8_linear_backward_tracks_bf16():
+    """E4M3 forward, data gradient and weight gradient (transpose-cast operands) of one projection."""
+    from kubeoperator_amd.ops import functional as kf
+
+    torch.manual_seed(2)
+    T, K, N = 1024, 2048, 4096
+    x0 = torch.randn(T, K, device="cuda", dtype=torch.bfloat16)
+    w0 = (torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16)
+    g = torch.randn(T, N, device="cuda", dtype=torch.bfloat16)
+    res = {}
+    for f8 in (False, True):
+        x = x0.clone().requires_grad_(True)
+        w = torch.nn.Parameter(w0.clone())
+        if f8:
+            _fp8_copies(w)
+        y = kf.linear(x, w)
+        y.backward(g)
+        res[f8] = (y.detach(), x.grad, w.grad)
+    for a, b in zip(res[True], res[False]):
+        assert _rel(a, b) < 0.06
+
+
+def test_fp8_swiglu_mlp_backward_tracks_bf16():
+    """All six GEMMs of the SwiGLU MLP in E4M3 (h^T and dgu^T cast with the forward / data-gradient scales)."""
+    from kubeoperator_amd.ops import functional as kf
+
+    torch.manual_seed(3)
+    T, H, F = 1024, 2048, 2048
+    x0 = torch.randn(T, H, device="cuda", dtype=torch.bfloat16)
+    wgu0 = (torch.randn(2 * F, H, device="cuda") * 0.02).to(torch.bfloat16)
+    wd0 = (torch.randn(H, F, device="cuda") * 0.02).to(torch.bfloat16)
+    g = torch.randn(T, H, device="cuda", dtype=torch.bfloat16)
+    res = {}
+    for f8 in (False, True):
+        x = x0.clone().requires_grad_(True)
+        wgu, wd = torch.nn.Parameter(wgu0.clone()), torch.nn.Parameter(wd0.clone())
+        if f8:
+            _fp8_copies(wgu)
+            _fp8_copies(wd)
+        y = kf.swiglu_mlp(x, wgu, wd)
+        y.backward(g)
+        res[f8] = (y.detach(), x.grad, wgu.grad, wd.grad)
+    for a, b in zip(res[True], res[False]):
+        assert _rel(a, b) < 0.08

@@ -18,6 +18,7 @@ GROUPS = [
     ("attn_fwd", re.compile(r"fa_fwd")),
     ("attn_bwd", re.compile(r"fa_bwd")),
     ("adamw", re.compile(r"adamw")),
+    ("fp8_quant", re.compile(r"fp8_(amax|cast)")),
     ("transpose", re.compile(r"transpose_(wide_)?kernel")),
     ("norm", re.compile(r"norm_|col_reduce")),
     ("swiglu/gelu", re.compile(r"swiglu|gelu")),  # incl. the fused transposed-output forms

@@ -217,9 +217,10 @@ void fp8_quant_(const Tensor& x, const Tensor& out, const Tensor& scale, const T
   check_gpu(amax_ws, "amax_ws");
   TORCH_CHECK(x.is_contiguous() && out.is_contiguous(), "fp8_quant: contiguous tensors only");
   TORCH_CHECK(out.element_size() == 1 && out.numel() == x.numel(), "fp8_quant: out must be 1-byte, x.numel()");
-  TORCH_CHECK(scale.numel() == 1 && amax_ws.nbytes() >= 4, "fp8_quant: scale / workspace size");
+  TORCH_CHECK(scale.numel() == 1 && amax_ws.nbytes() >= kop::kFp8AmaxBlocks * sizeof(float),
+              "fp8_quant: scale / workspace size");
   rc(kop::fp8_quantize(bp(x), x.numel(), reinterpret_cast<uint8_t*>(out.data_ptr()), scale.data_ptr<float>(),
-                       reinterpret_cast<unsigned*>(amax_ws.data_ptr()), cur_stream()),
+                       reinterpret_cast<float*>(amax_ws.data_ptr()), cur_stream()),
      "fp8_quant (x 16-byte and out 8-byte aligned)");
 }
 
@@ -352,6 +353,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cross_entropy_fwd_", &cross_entropy_fwd_);
   m.def("transpose_", &transpose_);
   m.def("fp8_quant_", &fp8_quant_);
+  m.attr("FP8_AMAX_BLOCKS") = kop::kFp8AmaxBlocks;
   m.def("fp8_cast_scaled_", &fp8_cast_scaled_);
   m.def("fp8_transpose_cast_", &fp8_transpose_cast_);
   m.def("adamw_", &adamw_);

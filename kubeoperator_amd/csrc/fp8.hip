@@ -5,10 +5,11 @@
 // quantized with "current scaling": scale = amax(|x|) / 448 (the E4M3 maximum), x8 = rne(x / scale), and the
 // GEMM multiplies the dequantization scales back in (torch._scaled_mm scale_a / scale_b).
 //
-// Two streaming passes: fp8_amax_kernel reduces |x| (one global atomic max per workgroup on the float's bit
-// pattern -- non-negative floats order like unsigned integers), then fp8_cast_kernel reads the amax, writes
-// the scale and converts 8 values per lane with v_cvt_pk_fp8_f32 (two per instruction) after clamping to
-// +-448, storing 8 bytes per lane. The second read of x mostly hits the 256 MB Infinity Cache.
+// Two streaming passes: fp8_amax_kernel reduces |x| to one partial maximum per workgroup (at most
+// kFp8AmaxBlocks of them: no atomics and no zeroed scratch, so no memset launch per quantization), then
+// fp8_cast_kernel reduces the partials in every workgroup, writes the scale and converts 8 values per lane
+// with v_cvt_pk_fp8_f32 (two per instruction) after clamping to +-448, storing 8 bytes per lane. The second
+// read of x mostly hits the 256 MB Infinity Cache.
 #include "common.h"
 #include "kernels.h"
 
@@ -19,8 +20,9 @@ constexpr float kE4M3Max = 448.f;
 constexpr int kBlock = 256;
 }  // namespace
 
+// Partial maxima, one per workgroup (no atomics, no zero-initialised scratch): the cast kernel reduces them.
 __global__ void __launch_bounds__(kBlock) fp8_amax_kernel(const bf16_t* __restrict__ x, int64_t n8, int64_t n,
-                                                          unsigned* __restrict__ amax) {
+                                                          float* __restrict__ partial) {
   __shared__ float red[kBlock / kWave];
   float m = 0.f;
   const u32x4* xv = reinterpret_cast<const u32x4*>(x);
@@ -33,7 +35,15 @@ __global__ void __launch_bounds__(kBlock) fp8_amax_kernel(const bf16_t* __restri
   if (blockIdx.x == 0)
     for (int64_t i = n8 * 8 + threadIdx.x; i < n; i += kBlock) m = fmaxf(m, fabsf(bf2f(x[i])));
   m = block_max<kBlock / kWave>(m, red);
-  if (threadIdx.x == 0) atomicMax(amax, __float_as_uint(m));
+  if (threadIdx.x == 0) partial[blockIdx.x] = m;
+}
+
+// amax over the partial maxima of fp8_amax_kernel (every workgroup reduces the few hundred floats itself)
+__device__ __forceinline__ float reduce_partials(const float* __restrict__ partial, int np) {
+  __shared__ float red[kBlock / kWave];
+  float m = 0.f;
+  for (int i = threadIdx.x; i < np; i += kBlock) m = fmaxf(m, partial[i]);
+  return block_max<kBlock / kWave>(m, red);
 }
 
 __device__ __forceinline__ uint32_t cvt4_fp8(float a, float b, float c, float d) {
@@ -43,9 +53,9 @@ __device__ __forceinline__ uint32_t cvt4_fp8(float a, float b, float c, float d)
 }
 
 __global__ void __launch_bounds__(kBlock) fp8_cast_kernel(const bf16_t* __restrict__ x, int64_t n8, int64_t n,
-                                                          const unsigned* __restrict__ amax,
+                                                          const float* __restrict__ partial, int np,
                                                           uint8_t* __restrict__ out, float* __restrict__ scale) {
-  const float a = __uint_as_float(*amax);
+  const float a = reduce_partials(partial, np);
   const float s = (a > 0.f && a < INFINITY) ? a / kE4M3Max : 1.f;
   const float inv = 1.f / s;
   if (blockIdx.x == 0 && threadIdx.x == 0) *scale = s;
@@ -158,14 +168,15 @@ int fp8_transpose_cast(const bf16_t* in, uint8_t* out, int64_t R, int64_t C, int
   return 0;
 }
 
-int fp8_quantize(const bf16_t* x, int64_t n, uint8_t* out, float* scale, unsigned* amax_ws, hipStream_t stream) {
+int fp8_quantize(const bf16_t* x, int64_t n, uint8_t* out, float* scale, float* partial_ws, hipStream_t stream) {
   if (n <= 0) return 0;
   if ((reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(out) & 7)) return -1;
   const int64_t n8 = n / 8;
+  int agrid = stream_grid(n8 > 0 ? n8 : 1, kBlock);
+  if (agrid > kFp8AmaxBlocks) agrid = kFp8AmaxBlocks;
   const int grid = stream_grid(n8 > 0 ? n8 : 1, kBlock);
-  (void)hipMemsetAsync(amax_ws, 0, sizeof(unsigned), stream);
-  fp8_amax_kernel<<<grid, kBlock, 0, stream>>>(x, n8, n, amax_ws);
-  fp8_cast_kernel<<<grid, kBlock, 0, stream>>>(x, n8, n, amax_ws, out, scale);
+  fp8_amax_kernel<<<agrid, kBlock, 0, stream>>>(x, n8, n, partial_ws);
+  fp8_cast_kernel<<<grid, kBlock, 0, stream>>>(x, n8, n, partial_ws, agrid, out, scale);
   KOP_CHECK_LAUNCH();
   return 0;
 }

@@ -47,8 +47,9 @@ int clip_coef(const float* sumsq, float max_norm, float* coef, float* norm_out, 
 int transpose2d(const bf16_t* in, bf16_t* out, int64_t R, int64_t C, int64_t ldi, int64_t ldo, hipStream_t stream);
 
 // fp8.hip: per-tensor OCP E4M3 quantization (current scaling): out = rne(clamp(x / scale)), scale = amax / 448;
-// amax_ws: one 4-byte device word of scratch
-int fp8_quantize(const bf16_t* x, int64_t n, uint8_t* out, float* scale, unsigned* amax_ws, hipStream_t stream);
+// partial_ws: kFp8AmaxBlocks floats of scratch
+constexpr int kFp8AmaxBlocks = 512;
+int fp8_quantize(const bf16_t* x, int64_t n, uint8_t* out, float* scale, float* partial_ws, hipStream_t stream);
 // cast with a known scale; transpose + cast (out[c][r] = e4m3(in[r][c] / scale))
 int fp8_cast_scaled(const bf16_t* x, int64_t n, const float* scale, uint8_t* out, hipStream_t stream);
 int fp8_transpose_cast(const bf16_t* in, uint8_t* out, int64_t R, int64_t C, int64_t ldi, int64_t ldo,

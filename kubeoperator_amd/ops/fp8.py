@@ -30,14 +30,14 @@ def quantize(x: torch.Tensor):
     x = x.contiguous()
     out = torch.empty(x.shape, dtype=FP8, device=x.device)
     scale = torch.empty((), dtype=torch.float32, device=x.device)
-    ws = torch.empty(1, dtype=torch.int32, device=x.device)
-    _lib().fp8_quant_(x, out.view(torch.uint8), scale, ws)
+    quantize_into(x, out, scale)
     return out, scale
 
 
 def quantize_into(x: torch.Tensor, out: torch.Tensor, scale: torch.Tensor) -> None:
-    ws = torch.empty(1, dtype=torch.int32, device=x.device)
-    _lib().fp8_quant_(x, out.view(torch.uint8), scale, ws)
+    lib = _lib()
+    ws = torch.empty(lib.FP8_AMAX_BLOCKS, dtype=torch.float32, device=x.device)  # per-workgroup partial maxima
+    lib.fp8_quant_(x, out.view(torch.uint8), scale, ws)
 
 
 def mm(a: torch.Tensor, b8_t: torch.Tensor, scale_b: torch.Tensor, out_dtype=torch.bfloat16) -> torch.Tensor:
@@ -69,6 +69,9 @@ def mm8(a8, sa, b8_t, sb, out_dtype=torch.bfloat16) -> torch.Tensor:
 def wgrad_into(dyt8: torch.Tensor, sdy: torch.Tensor, xt8: torch.Tensor, sx: torch.Tensor, out: torch.Tensor,
                accumulate: bool) -> None:
     """out (+)= dY^T X from the E4M3 transposed operands dY^T [N, T] and X^T [K, T]."""
+    if not accumulate and out.is_contiguous():
+        torch.ops.aten._scaled_mm.out(dyt8, xt8.t(), sdy, sx, None, None, out.dtype, False, out=out)
+        return
     res = torch._scaled_mm(dyt8, xt8.t(), scale_a=sdy, scale_b=sx, out_dtype=out.dtype)
     if accumulate:
         out.add_(res)

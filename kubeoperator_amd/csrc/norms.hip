@@ -197,15 +197,18 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(const bf16_t* __restrict_
   }
 }
 
-// Column reduce of [nparts, H] fp32 partials into a bf16 gradient (overwrite or accumulate). 16 row
-// segments per 64-column block and 8 independent partial sums per thread, so 8 loads are in flight (one
-// accumulator over 4 segments was a chain of dependent L2 round trips: 34 us for 512 x 4096).
+// Column reduce of [nparts, H] fp32 partials into a bf16 gradient (overwrite or accumulate). A block owns a
+// 16-column slab (64-byte row pieces) and splits the partial rows over 64 segments, 8 independent sums per
+// thread, so each thread has only nparts / 512 dependent L2 round trips. (The earlier 64-column blocks gave
+// H / 64 blocks -- 12 at GPT-2's 768 -- with nparts / 128 round trips each: 16 us for 2048 x 768.)
 __global__ void __launch_bounds__(1024) col_reduce_kernel(const float* __restrict__ part, int nparts, int H,
                                                           bf16_t* __restrict__ out, int accumulate) {
-  constexpr int SEG = 16;
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int seg = threadIdx.x >> 6;
-  __shared__ float red[SEG][64];
+  constexpr int CW = 16, SEG = 64;
+  const int cl = threadIdx.x & (CW - 1);
+  const int col = blockIdx.x * CW + cl;
+  const int seg = threadIdx.x / CW;
+  __shared__ float red[SEG][CW];
+  __shared__ float red8[8][CW];
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (col < H) {
     int p = seg;
@@ -213,18 +216,27 @@ __global__ void __launch_bounds__(1024) col_reduce_kernel(const float* __restric
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i] += part[(size_t)(p + i * SEG) * H + col];
     }
-    for (; p < nparts; p += SEG) acc[0] += part[(size_t)p * H + col];
+    for (int i = 0; p < nparts; p += SEG, i = (i + 1) & 7) acc[i] += part[(size_t)p * H + col];
   }
-  red[seg][threadIdx.x & 63] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  red[seg][cl] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  __syncthreads();
+  if (seg < 8) {  // 64 -> 8 segments
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += red[seg + 8 * i][cl];
+    red8[seg][cl] = t;
+  }
   __syncthreads();
   if (seg == 0 && col < H) {
     float t = 0.f;
 #pragma unroll
-    for (int i = 0; i < SEG; ++i) t += red[i][threadIdx.x];
+    for (int i = 0; i < 8; ++i) t += red8[i][cl];
     if (accumulate) t += bf2f(out[col]);
     out[col] = f2bf(t);
   }
 }
+
+static inline int col_reduce_blocks(int H) { return (H + 15) / 16; }
 
 // ---------------------------------------------------------------------------------------------------
 // Row-per-wave forward (H a multiple of 512, up to 4096 = Llama-3-8B): a 64-lane wave owns a whole row, each
@@ -300,6 +312,123 @@ __global__ void __launch_bounds__(256) norm_fwd_wave_kernel(const bf16_t* __rest
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Row-per-wave backward for NARROW rows (H = 256 * NC <= 1024: GPT-2's 768, 512 / 1024 widths). The block-per-
+// row kernel above moves only 1.5 KiB per tensor per row at H = 768 between two __syncthreads, so it is
+// latency-bound (~1 TB/s, 175 us for 32768 x 768). Here a wave owns a row: each lane holds NC 8-byte chunks
+// (4 bf16; chunk c = lane + 64c, one contiguous 512-byte wave access per c), the two row sums are wave
+// reductions, and the next row's loads are issued before the current row is computed. The weight-gradient
+// partials (12 fp32 per lane at H = 768, 16 at 1024) stay in registers across the rows of the wave and are
+// summed over the block's 4 waves in LDS once at the end: one fp32 partial row per block.
+// ---------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void unpack4(const u32x2 v, float* f) {
+  f[0] = __uint_as_float(v[0] << 16);
+  f[1] = __uint_as_float(v[0] & 0xffff0000u);
+  f[2] = __uint_as_float(v[1] << 16);
+  f[3] = __uint_as_float(v[1] & 0xffff0000u);
+}
+
+constexpr int kNarrowMaxH = 1024;
+constexpr int kNarrowMaxBlocks = 1024;
+
+template <int NC, bool LN, bool HAS_DRES>
+__global__ void __launch_bounds__(256) norm_bwd_narrow_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s,
+                                                              const bf16_t* __restrict__ w, const float* __restrict__ rstd_in,
+                                                              const float* __restrict__ mean_in,
+                                                              const bf16_t* __restrict__ dres, bf16_t* __restrict__ dx,
+                                                              float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                              int rows, int H) {
+  __shared__ f32x4 red[4 * kNarrowMaxH / 4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const float inv_h = 1.f / (float)H;
+  float wf[NC][4], dwa[NC][4], dba[NC][4];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    unpack4(reinterpret_cast<const u32x2*>(w)[lane + 64 * c], wf[c]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dwa[c][i] = dba[c][i] = 0.f;
+  }
+  const int stride = gridDim.x * 4;
+  int row = blockIdx.x * 4 + wv;
+  u32x2 sv[NC], dv[NC], rv[NC];
+  if (row < rows) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      sv[c] = reinterpret_cast<const u32x2*>(s + (size_t)row * H)[lane + 64 * c];
+      dv[c] = reinterpret_cast<const u32x2*>(dy + (size_t)row * H)[lane + 64 * c];
+      if (HAS_DRES) rv[c] = reinterpret_cast<const u32x2*>(dres + (size_t)row * H)[lane + 64 * c];
+    }
+  }
+  for (; row < rows; row += stride) {
+    u32x2 sc[NC], dc[NC], rc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      sc[c] = sv[c];
+      dc[c] = dv[c];
+      if (HAS_DRES) rc[c] = rv[c];
+    }
+    const float rstd = rstd_in[row];
+    const float mean = LN ? mean_in[row] : 0.f;
+    const int nxt = row + stride;
+    if (nxt < rows) {  // next row's loads in flight under this row's math
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        sv[c] = reinterpret_cast<const u32x2*>(s + (size_t)nxt * H)[lane + 64 * c];
+        dv[c] = reinterpret_cast<const u32x2*>(dy + (size_t)nxt * H)[lane + 64 * c];
+        if (HAS_DRES) rv[c] = reinterpret_cast<const u32x2*>(dres + (size_t)nxt * H)[lane + 64 * c];
+      }
+    }
+    float xh[NC][4], g[NC][4];
+    float a1 = 0.f, a2 = 0.f;  // sum(g*xhat), sum(g)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      float d[4];
+      unpack4(sc[c], xh[c]);
+      unpack4(dc[c], d);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        xh[c][i] = (xh[c][i] - mean) * rstd;
+        g[c][i] = d[i] * wf[c][i];
+        dwa[c][i] += d[i] * xh[c][i];
+        if (LN) dba[c][i] += d[i];
+        a1 += g[c][i] * xh[c][i];
+        a2 += g[c][i];
+      }
+    }
+    const float m1 = wave_sum(a1) * inv_h;
+    const float m2 = LN ? wave_sum(a2) * inv_h : 0.f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      float o[4], r[4];
+      if (HAS_DRES) unpack4(rc[c], r);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[i] = rstd * (g[c][i] - xh[c][i] * m1 - m2) + (HAS_DRES ? r[i] : 0.f);
+      reinterpret_cast<u32x2*>(dx + (size_t)row * H)[lane + 64 * c] = u32x2{pack2(o[0], o[1]), pack2(o[2], o[3])};
+    }
+  }
+  // the block's 4 wave partials -> one fp32 partial row (dw, then db)
+#pragma unroll
+  for (int pass = 0; pass < (LN ? 2 : 1); ++pass) {
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const float* a = pass ? dba[c] : dwa[c];
+      red[wv * (H >> 2) + lane + 64 * c] = f32x4{a[0], a[1], a[2], a[3]};
+    }
+    __syncthreads();
+    float* out = (pass ? db_part : dw_part) + (size_t)blockIdx.x * H;
+    for (int q = threadIdx.x; q < (H >> 2); q += 256) {
+      const int h4 = H >> 2;
+      reinterpret_cast<f32x4*>(out)[q] = (red[q] + red[h4 + q]) + (red[2 * h4 + q] + red[3 * h4 + q]);
+    }
+  }
+}
+
+static int narrow_nc(int H) {
+  if (H % 256 != 0 || H > kNarrowMaxH) return 0;
+  return H / 256;
+}
+
 // row-per-wave path: H = 512 * NV, NV in {1, 2, 4, 8}
 static int wave_nv(int H) {
   if (H % 512 != 0) return 0;
@@ -372,6 +501,10 @@ int norm_fwd(const bf16_t* x, const bf16_t* r, const bf16_t* w, const bf16_t* b,
 // Blocks of the backward = fp32 weight-gradient partial rows. Narrow rows (GPT-2's 768) need more blocks to
 // keep enough rows in flight: 512 blocks x 2 waves was latency-bound at ~1.5 TB/s.
 int norm_bwd_partial_rows(int rows, int H) {
+  if (narrow_nc(H)) {  // one partial row per 4-row-wave block
+    const int g = (rows + 3) / 4;
+    return g < kNarrowMaxBlocks ? g : kNarrowMaxBlocks;
+  }
   const int cap = H <= 1024 ? 2048 : 512;
   return rows < cap ? rows : cap;
 }
@@ -382,6 +515,25 @@ int norm_bwd(const bf16_t* dy, const bf16_t* s, const bf16_t* w, const float* rs
   if (H % 8 != 0 || H > 8192) return -1;
   const int grid = norm_bwd_partial_rows(rows, H);
   bool done = false;
+  if (const int nc = narrow_nc(H)) {
+#define NORM_BWD_NARROW(NCv)                                                                                 \
+    if (!done && nc == NCv) {                                                                                \
+      float* dbp = layernorm ? part + (size_t)grid * H : nullptr;                                            \
+      if (layernorm) {                                                                                       \
+        if (dres) norm_bwd_narrow_kernel<NCv, true, true><<<grid, 256, 0, stream>>>(dy, s, w, rstd, mean, dres, dx, part, dbp, rows, H); \
+        else norm_bwd_narrow_kernel<NCv, true, false><<<grid, 256, 0, stream>>>(dy, s, w, rstd, mean, dres, dx, part, dbp, rows, H); \
+      } else {                                                                                               \
+        if (dres) norm_bwd_narrow_kernel<NCv, false, true><<<grid, 256, 0, stream>>>(dy, s, w, rstd, mean, dres, dx, part, dbp, rows, H); \
+        else norm_bwd_narrow_kernel<NCv, false, false><<<grid, 256, 0, stream>>>(dy, s, w, rstd, mean, dres, dx, part, dbp, rows, H); \
+      }                                                                                                      \
+      done = true;                                                                                           \
+    }
+    NORM_BWD_NARROW(1)
+    NORM_BWD_NARROW(2)
+    NORM_BWD_NARROW(3)
+    NORM_BWD_NARROW(4)
+#undef NORM_BWD_NARROW
+  }
   int threads, nv;
   pick_geom(H, threads, nv);
   NORM_BWD_DISPATCH(1)
@@ -389,7 +541,7 @@ int norm_bwd(const bf16_t* dy, const bf16_t* s, const bf16_t* w, const float* rs
   NORM_BWD_DISPATCH(3)
   NORM_BWD_DISPATCH(4)
   if (!done) return -2;
-  const int cg = (H + 63) / 64;
+  const int cg = col_reduce_blocks(H);
   col_reduce_kernel<<<cg, 1024, 0, stream>>>(part, grid, H, dw, accumulate);
   if (layernorm) col_reduce_kernel<<<cg, 1024, 0, stream>>>(part + (size_t)grid * H, grid, H, db, accumulate);
   return 0;
@@ -459,7 +611,7 @@ int bias_grad(const bf16_t* dy, int rows, int H, float* part, bf16_t* db, int ac
   const int parts = bias_grad_parts(rows, H);
   const int per = (rows + parts - 1) / parts;
   bias_partial_kernel<<<dim3((H / 8 + 63) / 64, parts), 256, 0, stream>>>(dy, rows, H, per, part);
-  col_reduce_kernel<<<(H + 63) / 64, 1024, 0, stream>>>(part, parts, H, db, accumulate);
+  col_reduce_kernel<<<col_reduce_blocks(H), 1024, 0, stream>>>(part, parts, H, db, accumulate);
   return 0;
 }
 

@@ -61,25 +61,34 @@ def test_rmsnorm_fwd_bwd(H, with_res):
         assert rel_err(r.grad, rf.grad) < 3e-2
 
 
-@pytest.mark.parametrize("H", [768, 4096])
-def test_layernorm_fwd_bwd(H):
+@pytest.mark.parametrize("H,T,with_res", [(768, 257, False), (4096, 257, False), (768, 9001, True),
+                                          (512, 4099, True), (1024, 3, False)])
+def test_layernorm_fwd_bwd(H, T, with_res):
+    """H <= 1024 takes the row-per-wave narrow backward (several rows per wave once T > 4096 rows)."""
     from kubeoperator_amd.ops.functional import layer_norm
 
     torch.manual_seed(1)
-    T = 257
     x = (torch.randn(T, H, device=DEV) * 2 + 0.5).to(torch.bfloat16).requires_grad_(True)
+    r = torch.randn(T, H, device=DEV, dtype=torch.bfloat16, requires_grad=True) if with_res else None
     w = (1 + 0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16).requires_grad_(True)
     b = (0.1 * torch.randn(H, device=DEV)).to(torch.bfloat16).requires_grad_(True)
-    y = layer_norm(x, w, b, 1e-5)
+    out = layer_norm(x, w, b, 1e-5, residual=r)
+    y, s = out if with_res else (out, None)
     dy = torch.randn_like(y)
-    (y.float() * dy.float()).sum().backward()
+    ds = torch.randn_like(y) if with_res else None
+    ((y.float() * dy.float()).sum() + ((s.float() * ds.float()).sum() if with_res else 0)).backward()
     xf, wf, bf = (t.detach().float().requires_grad_(True) for t in (x, w, b))
-    yf = torch.nn.functional.layer_norm(xf, (H,), wf, bf, 1e-5)
-    (yf * dy.float()).sum().backward()
+    rf = r.detach().float().requires_grad_(True) if with_res else None
+    sf = xf + rf if with_res else xf
+    sf_b = sf.to(torch.bfloat16).float() if with_res else sf
+    yf = torch.nn.functional.layer_norm(sf_b, (H,), wf, bf, 1e-5)
+    ((yf * dy.float()).sum() + ((sf * ds.float()).sum() if with_res else 0)).backward()
     assert rel_err(y, yf) < 2e-2
     assert rel_err(x.grad, xf.grad) < 3e-2
     assert rel_err(w.grad, wf.grad) < 3e-2
     assert rel_err(b.grad, bf.grad) < 3e-2
+    if with_res:
+        assert rel_err(r.grad, rf.grad) < 3e-2
 
 
 @pytest.mark.parametrize("D", [128, 64])

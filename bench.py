@@ -59,6 +59,9 @@ def main() -> int:
     ap.add_argument("--cuda-graph", type=int, default=0, choices=[0, 1],
                     help="replay each micro-batch's forward + backward as a captured HIP graph (one GPU only; pays "
                          "off when small micro-batches are bound by host-side launch overhead)")
+    ap.add_argument("--tp", type=int, default=1,
+                    help="tensor-parallel degree (Llama; TP groups of consecutive ranks, DP across them). The "
+                         "headline runs tp 1: Llama-3-8B and its fp32 optimizer state fit one MI355X")
     args = ap.parse_args()
 
     import torch
@@ -81,9 +84,11 @@ def main() -> int:
                      overlap_optimizer=bool(args.overlap_opt),
                      transposed_weights=os.environ.get("KOP_TRANSPOSED_W", "1") != "0",
                      cuda_graph=bool(args.cuda_graph), grad_dtype=args.grad_dtype,
-                     wgrad_stream=args.wgrad_stream, recompute=bool(args.recompute), fp8=bool(args.fp8))
+                     wgrad_stream=args.wgrad_stream, recompute=bool(args.recompute), fp8=bool(args.fp8), tp=args.tp)
     trainer = Trainer(tc, info)
-    data = SyntheticTokens(trainer.cfg.vocab_size, args.mbs, args.seq, info.device, seed=tc.seed, rank=info.rank)
+    dp_world = trainer.dp_info.world
+    data = SyntheticTokens(trainer.cfg.vocab_size, args.mbs, args.seq, info.device, seed=tc.seed,
+                           rank=trainer.dp_info.rank)
     cuda = info.device.type == "cuda"
 
     def sync():
@@ -106,7 +111,7 @@ def main() -> int:
     elapsed = all_reduce_max(elapsed, info)
     gemm_tuning.finish(tuning, info.rank)
     last_loss = float(loss.item()) if loss is not None else float("nan")
-    tokens = world * trainer.tokens_per_step * args.steps
+    tokens = trainer.job_tokens_per_step * args.steps
     value = tokens / elapsed
     ms = elapsed / args.steps * 1000.0
     cfg = trainer.cfg
@@ -131,11 +136,12 @@ def main() -> int:
             "config": {
                 "model": model_name,
                 "params": cfg.num_params(),
-                "global_batch": args.mbs * args.accum * world,
+                "global_batch": args.mbs * args.accum * dp_world,
                 "micro_batch_per_gpu": args.mbs,
                 "grad_accum": args.accum,
                 "seq_len": args.seq,
-                "parallelism": f"dp{world}" + ("-zero1" if args.dp == "zero1" and world > 1 else ""),
+                "parallelism": (f"tp{args.tp}-" if args.tp > 1 else "") + f"dp{dp_world}"
+                + ("-zero1" if args.dp == "zero1" and dp_world > 1 else ""),
                 "optimizer": "fused AdamW (fp32 master/moments), grad clip 1.0",
                 "optimizer_overlap": bool(args.overlap_opt),
                 "hip_graph": bool(args.cuda_graph),

@@ -4,10 +4,13 @@ from .gpt2 import GPT2
 from .llama import Llama
 
 
-def build_model(cfg: ModelConfig):
+def build_model(cfg: ModelConfig, tp=None):
+    """``tp``: a ``parallel.tensor.TPContext`` (tensor parallelism is implemented for the Llama family)."""
     if cfg.arch == "llama":
-        return Llama(cfg)
+        return Llama(cfg, tp)
     if cfg.arch == "gpt2":
+        if tp is not None and tp.size > 1:
+            raise ValueError("tensor parallelism is implemented for the Llama family")
         return GPT2(cfg)
     raise ValueError(f"unknown architecture {cfg.arch}")
 

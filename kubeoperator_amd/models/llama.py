@@ -14,6 +14,9 @@ every elementwise/normalisation kernel streams contiguous rows. Per block:
 With ``recompute`` each block keeps only its inputs for backward and re-runs its forward there (one more
 forward pass, ~1/3 more FLOPs): what lets one MI355X train Llama-3-8B at 32k-token sequences.
 
+With tensor parallelism (``tp``, ``parallel.tensor``) each block holds its TP rank's heads of Wqkv / Wo and
+its slice of the FFN (gate|up rows, down columns); the two row-split projections end in a TP all-reduce.
+
 The LM head and the cross-entropy are one autograd node whose logits buffer is overwritten by its own
 gradient (``ops.cross_entropy_lmhead``). Weight gradients are written straight into the flat gradient
 buffer (see ``parallel.flat``).
@@ -29,41 +32,47 @@ from torch.utils.checkpoint import checkpoint
 from ..ops import functional as kf
 from ..ops.reference import rope_cache
 from ..parallel.flat import ParamSpec
+from ..parallel.tensor import TPContext, check_llama_tp, copy_to_tp, reduce_from_tp
 from .config import ModelConfig
 
 
 class LlamaBlock(nn.Module):
-    def __init__(self, cfg: ModelConfig):
+    def __init__(self, cfg: ModelConfig, tp: TPContext | None = None):
         super().__init__()
+        self.tp = tp or TPContext()
+        t = self.tp.size
         H, D = cfg.hidden, cfg.head_dim
         self.cfg = cfg
+        self.hq, self.hkv, self.ffn = cfg.n_heads // t, cfg.n_kv_heads // t, cfg.ffn_hidden // t  # this rank's
         self.attn_norm = nn.Parameter(torch.empty(H))
-        self.wqkv = nn.Parameter(torch.empty((cfg.n_heads + 2 * cfg.n_kv_heads) * D, H))
-        self.wo = nn.Parameter(torch.empty(H, cfg.n_heads * D))
+        self.wqkv = nn.Parameter(torch.empty((self.hq + 2 * self.hkv) * D, H))
+        self.wo = nn.Parameter(torch.empty(H, self.hq * D))
         self.mlp_norm = nn.Parameter(torch.empty(H))
-        self.w_gate_up = nn.Parameter(torch.empty(2 * cfg.ffn_hidden, H))
-        self.w_down = nn.Parameter(torch.empty(H, cfg.ffn_hidden))
+        self.w_gate_up = nn.Parameter(torch.empty(2 * self.ffn, H))
+        self.w_down = nn.Parameter(torch.empty(H, self.ffn))
 
     def forward(self, x, pending, cos, sin, B, S):
-        c = self.cfg
+        c, tp = self.cfg, self.tp
         if pending is None:
             y, x1 = kf.rms_norm(x, self.attn_norm, c.norm_eps), x
         else:
             y, x1 = kf.rms_norm(x, self.attn_norm, c.norm_eps, residual=pending)
-        qkv = kf.linear(y, self.wqkv)
-        a = kf.rope_attention(qkv, cos, sin, B, S, c.n_heads, c.n_kv_heads, c.head_dim, causal=True)
-        a = kf.linear(a, self.wo)
+        qkv = kf.linear(copy_to_tp(y, tp), self.wqkv)
+        a = kf.rope_attention(qkv, cos, sin, B, S, self.hq, self.hkv, c.head_dim, causal=True)
+        a = reduce_from_tp(kf.linear(a, self.wo), tp)
         y2, x2 = kf.rms_norm(x1, self.mlp_norm, c.norm_eps, residual=a)
-        return x2, kf.swiglu_mlp(y2, self.w_gate_up, self.w_down)
+        return x2, reduce_from_tp(kf.swiglu_mlp(copy_to_tp(y2, tp), self.w_gate_up, self.w_down), tp)
 
 
 class Llama(nn.Module):
-    def __init__(self, cfg: ModelConfig):
+    def __init__(self, cfg: ModelConfig, tp: TPContext | None = None):
         super().__init__()
         assert cfg.arch == "llama"
+        self.tp = tp or TPContext()
+        check_llama_tp(cfg, self.tp.size)
         self.cfg = cfg
         self.tok_emb = nn.Parameter(torch.empty(cfg.vocab_size, cfg.hidden))
-        self.layers = nn.ModuleList([LlamaBlock(cfg) for _ in range(cfg.n_layers)])
+        self.layers = nn.ModuleList([LlamaBlock(cfg, self.tp) for _ in range(cfg.n_layers)])
         self.final_norm = nn.Parameter(torch.empty(cfg.hidden))
         if not cfg.tie_embeddings:
             self.lm_head = nn.Parameter(torch.empty(cfg.vocab_size, cfg.hidden))
@@ -75,16 +84,17 @@ class Llama(nn.Module):
         c = self.cfg
         std = c.init_std
         out_std = std / math.sqrt(2 * c.n_layers)
+        sh = self.tp.enabled  # block projections are TP shards
         specs = []
         if not c.tie_embeddings:
             specs.append(ParamSpec("lm_head", self.lm_head, True, 1, "normal", std))
         for i in reversed(range(c.n_layers)):
             L = self.layers[i]
             specs += [
-                ParamSpec(f"layers.{i}.w_down", L.w_down, True, 1, "normal", out_std),
-                ParamSpec(f"layers.{i}.w_gate_up", L.w_gate_up, True, 1, "normal", std),
-                ParamSpec(f"layers.{i}.wo", L.wo, True, 1, "normal", out_std),
-                ParamSpec(f"layers.{i}.wqkv", L.wqkv, True, 1, "normal", std),
+                ParamSpec(f"layers.{i}.w_down", L.w_down, True, 1, "normal", out_std, sh),
+                ParamSpec(f"layers.{i}.w_gate_up", L.w_gate_up, True, 1, "normal", std, sh),
+                ParamSpec(f"layers.{i}.wo", L.wo, True, 1, "normal", out_std, sh),
+                ParamSpec(f"layers.{i}.wqkv", L.wqkv, True, 1, "normal", std, sh),
             ]
         specs.append(ParamSpec("tok_emb", self.tok_emb, True, 2 if c.tie_embeddings else 1, "normal", std))
         specs.append(ParamSpec("final_norm", self.final_norm, False, 1, "ones"))

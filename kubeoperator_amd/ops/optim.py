@@ -27,6 +27,7 @@ class Segment:
     grad: torch.Tensor   # bf16 view (flat), same numel
     weight_decay: float
     bucket: int = -1     # flat-store bucket this segment belongs to (for overlap gates)
+    norm_weight: float = 1.0  # weight of its sum of squares in the global grad norm (1/tp: TP-replicated)
 
 
 class FusedAdamW:
@@ -59,6 +60,10 @@ class FusedAdamW:
             self._views.append((off, off + k))
             off += k
         self._sumsq = torch.zeros(1, dtype=torch.float32, device=dev)
+        self._sumsq_w = torch.zeros(1, dtype=torch.float32, device=dev)  # segments with norm_weight != 1
+        self._norm_w = {s.norm_weight for s in segments if s.norm_weight != 1.0}
+        if len(self._norm_w) > 1:
+            raise ValueError("one replicated-segment norm weight per optimizer")
         self._coef = torch.ones(1, dtype=torch.float32, device=dev)
         self.last_grad_norm = torch.zeros(1, dtype=torch.float32, device=dev)
         self.store = store
@@ -79,16 +84,21 @@ class FusedAdamW:
             self._coef.fill_(1.0)
             return
         self._sumsq.zero_()
+        if self._norm_w:
+            self._sumsq_w.zero_()
         if self._native():
             from . import load
 
             lib = load()
             for s in self.segments:
                 if s.grad.numel():
-                    lib.grad_sumsq_(s.grad.reshape(-1), self._sumsq)
+                    lib.grad_sumsq_(s.grad.reshape(-1), self._sumsq if s.norm_weight == 1.0 else self._sumsq_w)
         else:
             for s in self.segments:
-                self._sumsq += s.grad.float().pow(2).sum()
+                acc = self._sumsq if s.norm_weight == 1.0 else self._sumsq_w
+                acc += s.grad.float().pow(2).sum()
+        if self._norm_w:  # TP-replicated gradients: every TP rank holds a copy, counted once after the sum
+            self._sumsq.add_(self._sumsq_w, alpha=next(iter(self._norm_w)))
         if self.grad_scale != 1.0:
             self._sumsq.mul_(self.grad_scale * self.grad_scale)
         if self.norm_allreduce is not None:
@@ -157,6 +167,11 @@ class FusedAdamW:
                 w.mul_(1 - lr * s.weight_decay)
                 w.sub_(lr * (m / bc1) / (v.sqrt() / math.sqrt(bc2) + self.eps))
                 s.param.reshape(-1).copy_(w)
+
+    def sync_master(self) -> None:
+        """Re-derive the fp32 master weights from the bf16 parameters (after parameters were loaded)."""
+        for s, (a, b) in zip(self.segments, self._views):
+            self.master[a:b].copy_(s.param.reshape(-1).float())
 
     # checkpointing -------------------------------------------------------------------------------
     def state_dict(self):

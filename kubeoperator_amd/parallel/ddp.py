@@ -30,11 +30,16 @@ from .flat import Bucket, FlatParamStore
 
 
 class DataParallel:
-    def __init__(self, store: FlatParamStore, info: DistInfo, mode: str = "allreduce"):
+    """``info`` is the data-parallel view of this rank: the whole job, or under tensor parallelism the ranks
+    with this rank's TP index (``info.group``; ``tp`` the ``parallel.tensor.TPContext``)."""
+
+    def __init__(self, store: FlatParamStore, info: DistInfo, mode: str = "allreduce", tp=None):
         if mode not in ("allreduce", "zero1"):
             raise ValueError(f"unknown data-parallel mode {mode!r}")
         self.store = store
         self.info = info
+        self.group = info.group
+        self.tp = tp
         self.mode = mode
         self.world = info.world
         self.rank = info.rank
@@ -48,7 +53,7 @@ class DataParallel:
     # -------------------------------------------------------------------------------------------
     def broadcast_params(self) -> None:
         if self.world > 1:
-            dist.broadcast(self.store.params, src=0)
+            dist.broadcast(self.store.params, src=self.info.src, group=self.group)
 
     def _on_ready(self, b: Bucket) -> None:
         if self.world == 1 or not self.sync:
@@ -56,10 +61,10 @@ class DataParallel:
         g = self.store.grads[b.start:b.end]
         self.comm_bytes += g.numel() * g.element_size()
         if self.mode == "allreduce":
-            self._works.append(dist.all_reduce(g, async_op=True))
+            self._works.append(dist.all_reduce(g, group=self.group, async_op=True))
         else:
             a, e = b.piece(self.rank, self.world)
-            self._works.append(dist.reduce_scatter_tensor(self.store.grads[a:e], g, async_op=True))
+            self._works.append(dist.reduce_scatter_tensor(self.store.grads[a:e], g, group=self.group, async_op=True))
 
     def finish_grads(self) -> None:
         """Make the current (compute) stream wait for every outstanding gradient collective."""
@@ -74,10 +79,12 @@ class DataParallel:
     def optimizer_segments(self) -> list[Segment]:
         st = self.store
         wd_of = {True: None, False: 0.0}
+        rep_w = 1.0 / self.tp.size if self.tp is not None and self.tp.enabled else 1.0
         segs = []
         for b in st.buckets:
             a, e = (b.start, b.end) if self.mode == "allreduce" or self.world == 1 else b.piece(self.rank, self.world)
-            segs.append(Segment(st.params[a:e], st.grads[a:e], wd_of[b.decay], b.index))
+            segs.append(Segment(st.params[a:e], st.grads[a:e], wd_of[b.decay], b.index,
+                                1.0 if b.shard else rep_w))
         return segs
 
     def publish_segment(self, seg: Segment):
@@ -99,11 +106,18 @@ class DataParallel:
         ``copy_`` at ``wait()``, i.e. mid-forward when the gate is resolved). The ordering that matters --
         bucket Y written before any kernel reads it -- is the gate's stream dependency, not autograd's."""
         pd = self.store.params.data
-        return dist.all_gather_into_tensor(pd[b.start:b.end], pd[a:e], async_op=async_op)
+        return dist.all_gather_into_tensor(pd[b.start:b.end], pd[a:e], group=self.group, async_op=async_op)
 
     def norm_allreduce(self):
+        """The grad-norm sum of squares is summed over the ranks holding distinct gradient pieces: the DP
+        group under ZeRO-1, the TP group under tensor parallelism, the whole job with both."""
+        tp = self.tp is not None and self.tp.enabled
         if self.mode == "zero1" and self.world > 1:
-            return lambda t: dist.all_reduce(t)
+            if tp:
+                return lambda t: dist.all_reduce(t)  # every rank: DP pieces x TP shards
+            return lambda t: dist.all_reduce(t, group=self.group)
+        if tp:
+            return lambda t: dist.all_reduce(t, group=self.tp.group)
         return None
 
     def after_step(self) -> None:

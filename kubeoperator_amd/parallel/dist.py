@@ -20,6 +20,11 @@ class DistInfo:
     world: int = 1
     backend: str = "none"
     device: torch.device = torch.device("cpu")
+    # a sub-group view (the data-parallel ranks of a tensor-parallel job, parallel.tensor): rank / world are
+    # within ``group``, ``src`` is the global rank of the group's rank 0, ``global_rank`` this process's rank in the whole job
+    group: object = None
+    src: int = 0
+    global_rank: int = -1
 
     @property
     def is_main(self) -> bool:
@@ -70,16 +75,16 @@ def init_distributed(device: str = "auto", timeout_s: int = 1800) -> DistInfo:
 def barrier(info: DistInfo) -> None:
     if info.world > 1:
         if info.backend == "nccl":
-            dist.barrier(device_ids=[info.local_rank])
+            dist.barrier(group=info.group, device_ids=[info.local_rank])
         else:
-            dist.barrier()
+            dist.barrier(group=info.group)
 
 
 def all_reduce_max(x: float, info: DistInfo) -> float:
     if info.world == 1:
         return x
     t = torch.tensor([x], dtype=torch.float64, device=info.device if info.backend == "nccl" else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=info.group)
     return float(t.item())
 
 
@@ -87,7 +92,7 @@ def all_reduce_sum(x: float, info: DistInfo) -> float:
     if info.world == 1:
         return x
     t = torch.tensor([x], dtype=torch.float64, device=info.device if info.backend == "nccl" else "cpu")
-    dist.all_reduce(t)
+    dist.all_reduce(t, group=info.group)
     return float(t.item())
 
 

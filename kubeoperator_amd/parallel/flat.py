@@ -46,6 +46,7 @@ class ParamSpec:
     uses: int = 1
     init: str = "normal"  # normal | ones | zeros | normal_scaled
     std: float = 0.02
+    shard: bool = False  # tensor-parallel shard (parallel.tensor): own buckets, own init stream per TP rank
 
 
 @dataclass
@@ -57,6 +58,7 @@ class Bucket:
     expected: int = 0
     pending: int = 0
     decay: bool = True
+    shard: bool = False  # holds tensor-parallel shards (replicated parameters never share its bucket)
 
     @property
     def numel(self) -> int:
@@ -128,11 +130,11 @@ class FlatParamStore:
             cur = None
             for s in region:
                 n = s.param.numel()
-                if cur is not None and (cur.end - cur.start) + n > cap:
+                if cur is not None and ((cur.end - cur.start) + n > cap or cur.shard != s.shard):
                     off = close(cur)
                     cur = None
                 if cur is None:
-                    cur = Bucket(len(self.buckets), off, off, decay=is_decay)
+                    cur = Bucket(len(self.buckets), off, off, decay=is_decay, shard=s.shard)
                 offsets[s.name] = cur.end
                 cur.end = _round_up(cur.end + n, ALIGN)
                 cur.names.append(s.name)
@@ -196,10 +198,14 @@ class FlatParamStore:
         return self._param_by_name.items()
 
     # -------------------------------------------------------------------------------------------
-    def init_weights(self, seed: int = 0) -> None:
-        """Initialise every parameter in place on its device (no host round trip at 8B params)."""
+    def init_weights(self, seed: int = 0, shard_rank: int = 0) -> None:
+        """Initialise every parameter in place on its device (no host round trip at 8B params). Tensor-parallel
+        shards draw from a stream seeded by their TP rank; replicated parameters from one stream every rank
+        shares (so they start identical across the TP group)."""
         g = torch.Generator(device=self.device)
         g.manual_seed(seed)
+        gs = torch.Generator(device=self.device)
+        gs.manual_seed(seed + 7919 * (shard_rank + 1))
         with torch.no_grad():
             for name, p in self._param_by_name.items():
                 s = self.specs[name]
@@ -208,7 +214,7 @@ class FlatParamStore:
                 elif s.init == "zeros":
                     p.zero_()
                 else:
-                    p.normal_(0.0, s.std, generator=g)
+                    p.normal_(0.0, s.std, generator=gs if s.shard else g)
 
     def reset_readiness(self) -> None:
         for b in self.buckets:

@@ -12,6 +12,10 @@ a checkpoint written at another world size. Every file carries its flat layout (
 where each optimizer-state segment sits); the loader memory-maps the old ranks' files and copies, per
 parameter, the intersection of the old pieces with this rank's new segments -- each rank reads only its own
 new shard of the fp32 state (12 B/param / world), never the whole 96 GB of an 8B model.
+
+Tensor parallelism: TP rank t of T keeps its own tree ``<dir>/tp<t>_of<T>/`` written by its data-parallel
+group (the shards differ per TP rank); resuming needs the same TP degree, the DP size may change (the
+reshard above runs inside each TP rank's tree). A resume takes the newest step complete in EVERY tree.
 """
 from __future__ import annotations
 
@@ -23,7 +27,18 @@ import torch
 from ..parallel.dist import DistInfo, barrier
 
 
+def _tp_view(trainer, directory: str, info: DistInfo):
+    """(directory, data-parallel info) of this rank's checkpoint tree."""
+    tp = getattr(trainer, "tp", None)
+    if tp is None or not tp.enabled:
+        return directory, info
+    return os.path.join(directory, f"tp{tp.rank}_of{tp.size}"), trainer.dp_info
+
+
 def save(trainer, directory: str, info: DistInfo) -> str:
+    job = info
+    directory, info = _tp_view(trainer, directory, info)
+    os.makedirs(directory, exist_ok=True)
     step = trainer.step
     d = os.path.join(directory, f"step_{step}")
     os.makedirs(d, exist_ok=True)
@@ -38,7 +53,7 @@ def save(trainer, directory: str, info: DistInfo) -> str:
         with open(os.path.join(directory, "latest.tmp"), "w") as f:
             f.write(str(step))
         os.replace(os.path.join(directory, "latest.tmp"), os.path.join(directory, "latest"))
-    barrier(info)
+    barrier(job)
     return d
 
 
@@ -56,7 +71,17 @@ def _files(d: str) -> list[str]:
 
 
 def load(trainer, directory: str, info: DistInfo, step: int | None = None) -> int | None:
-    step = latest_step(directory) if step is None else step
+    job = info
+    directory, info = _tp_view(trainer, directory, info)
+    if step is None:
+        step = latest_step(directory)
+        if info is not job:  # TP: the newest step every TP rank's tree completed
+            import torch.distributed as dist
+
+            t = torch.tensor([-1 if step is None else step], dtype=torch.int64,
+                             device=job.device if job.backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            step = None if int(t) < 0 else int(t)
     if step is None:
         return None
     d = os.path.join(directory, f"step_{step}")

@@ -47,6 +47,8 @@ def main(argv=None) -> int:
                     help="gradient buffer precision (fp32: accumulation and DP reduction in fp32)")
     ap.add_argument("--cuda-graph", type=int, default=0, choices=[0, 1],
                     help="replay micro-batches as captured HIP graphs (one GPU; small micro-batches)")
+    ap.add_argument("--tp", type=int, default=1,
+                    help="tensor-parallel degree (Llama): TP groups of consecutive ranks, data parallelism across them")
     ap.add_argument("--metrics-port", type=int, default=0, help="rank 0 serves Prometheus metrics here (0: off)")
     ap.add_argument("--inject-fault", default="",
                     help="fault injection 'RANK:STEP': that rank dies abruptly after finishing STEP (before its "
@@ -74,16 +76,17 @@ def main(argv=None) -> int:
     tc = TrainConfig(model=a.model, micro_batch=a.mbs, seq_len=a.seq, grad_accum=a.accum, lr=a.lr,
                      warmup_steps=a.warmup, total_steps=a.steps, dp_mode=a.dp, bucket_mb=a.bucket_mb, overlap_optimizer=bool(a.overlap_opt),
                      cuda_graph=bool(a.cuda_graph), grad_dtype=a.grad_dtype,
-                     wgrad_stream=a.wgrad_stream, recompute=bool(a.recompute), fp8=bool(a.fp8))
+                     wgrad_stream=a.wgrad_stream, recompute=bool(a.recompute), fp8=bool(a.fp8), tp=a.tp)
     tr = Trainer(tc, info)
+    dpi = tr.dp_info  # the TP ranks of a group read the same tokens
     if a.resume and a.ckpt_dir:
         s = checkpoint.load(tr, a.ckpt_dir, info)
         if s is not None and info.is_main:
             print(json.dumps({"event": "resumed", "step": s}), flush=True)
     if a.data == "synthetic":
-        data = SyntheticTokens(tr.cfg.vocab_size, a.mbs, a.seq, info.device, seed=tc.seed + tr.step, rank=info.rank)
+        data = SyntheticTokens(tr.cfg.vocab_size, a.mbs, a.seq, info.device, seed=tc.seed + tr.step, rank=dpi.rank)
     else:
-        data = TokenFileDataset(a.data, a.mbs, a.seq, info.device, seed=tc.seed, rank=info.rank, world=info.world,
+        data = TokenFileDataset(a.data, a.mbs, a.seq, info.device, seed=tc.seed, rank=dpi.rank, world=dpi.world,
                                 start_batch=tr.step * a.accum)
     cuda = info.device.type == "cuda"
     flops_tok = tr.cfg.flops_per_token(a.seq)
@@ -100,7 +103,7 @@ def main(argv=None) -> int:
             if cuda:
                 torch.cuda.synchronize()
             dt = all_reduce_max(time.perf_counter() - t0, info)
-            toks = info.world * tr.tokens_per_step / dt
+            toks = tr.job_tokens_per_step / dt
             if info.is_main:
                 rec = {"step": tr.step, "loss": round(float(loss), 4),
                        "grad_norm": round(float(tr.opt.last_grad_norm), 4),

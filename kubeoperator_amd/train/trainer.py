@@ -18,6 +18,7 @@ from ..ops.optim import FusedAdamW
 from ..parallel.ddp import DataParallel
 from ..parallel.dist import DistInfo
 from ..parallel.flat import FlatParamStore
+from ..parallel.tensor import check_llama_tp, make_groups
 
 
 @dataclass
@@ -43,6 +44,7 @@ class TrainConfig:
     fp8: bool = False  # E4M3 forward + data-gradient GEMMs of the block projections (ops/fp8.py; opt-in)
     recompute: bool = False  # per-block activation recompute (long sequences: only block inputs stay saved)
     wgrad_stream: str = "auto"  # weight-gradient GEMMs on a side stream: auto (narrow models, hidden < 2048) | on | off
+    tp: int = 1  # tensor-parallel degree (Llama; TP groups of consecutive ranks, DP across them: parallel.tensor)
     seed: int = 1234
     model_overrides: dict = field(default_factory=dict)
 
@@ -61,6 +63,9 @@ class Trainer:
     def __init__(self, tc: TrainConfig, info: DistInfo):
         self.tc = tc
         self.info = info
+        # data-parallel view of this rank + its tensor-parallel group (the whole job and no TP when tp == 1)
+        check_llama_tp(get_config(tc.model, **tc.model_overrides), tc.tp)
+        self.dp_info, self.tp = make_groups(info, tc.tp)
         overrides = dict(tc.model_overrides)
         base = get_config(tc.model)
         if tc.seq_len > base.max_seq_len and base.arch == "llama" and "max_seq_len" not in overrides:
@@ -72,15 +77,15 @@ class Trainer:
         dev = info.device
         t0 = time.time()
         with torch.device("meta"):
-            self.model = build_model(self.cfg)
+            self.model = build_model(self.cfg, self.tp)
         self.model.recompute = bool(tc.recompute)
         if tc.grad_dtype not in ("bf16", "fp32"):
             raise ValueError(f"grad_dtype must be bf16 or fp32, not {tc.grad_dtype!r}")
-        self.store = FlatParamStore(self.model, self.model.param_specs(), dev, world=info.world,
+        self.store = FlatParamStore(self.model, self.model.param_specs(), dev, world=self.dp_info.world,
                                     bucket_bytes=tc.bucket_mb * 1024 * 1024,
                                     grad_dtype=torch.float32 if tc.grad_dtype == "fp32" else torch.bfloat16)
-        self.store.init_weights(seed=tc.seed)
-        self.dp = DataParallel(self.store, info, tc.dp_mode)
+        self.store.init_weights(seed=tc.seed, shard_rank=self.tp.rank)
+        self.dp = DataParallel(self.store, self.dp_info, tc.dp_mode, self.tp)
         self.dp.broadcast_params()
         if tc.transposed_weights and dev.type == "cuda":
             self.store.enable_transposed()
@@ -112,8 +117,13 @@ class Trainer:
 
     @property
     def tokens_per_step(self) -> int:
-        """Tokens processed per optimizer step by THIS rank."""
+        """Tokens processed per optimizer step by THIS rank (its TP group shares them)."""
         return self.tc.micro_batch * self.tc.seq_len * self.tc.grad_accum
+
+    @property
+    def job_tokens_per_step(self) -> int:
+        """Tokens per optimizer step of the whole job: one micro-batch stream per data-parallel rank."""
+        return self.dp_info.world * self.tokens_per_step
 
     def train_step(self, batches) -> torch.Tensor:
         """``batches``: iterable of ``grad_accum`` (ids, targets) pairs, each [micro_batch, seq_len]."""
@@ -164,6 +174,20 @@ class Trainer:
         self._graphs[key].replay()
         return self._graph_loss[key].clone()
 
+    def load_full_weights(self, full: dict) -> None:
+        """Load unsharded (tp = 1) weights by name: each TP rank keeps its slice (``parallel.tensor``). The
+        fp32 masters and the derived weight copies follow. Weight conversion into a TP job, and the TP tests."""
+        from ..parallel.tensor import shard_llama_weight
+
+        self.store.await_all()
+        with torch.no_grad():
+            for name, p in self.store.named_params():
+                w = shard_llama_weight(name, full[name], self.cfg, self.tp.size, self.tp.rank)
+                p.copy_(w.to(device=p.device, dtype=p.dtype))
+        self.opt.sync_master()
+        self.store.refresh_transposed()
+        self.store.refresh_fp8()
+
     # checkpoint -----------------------------------------------------------------------------------
     def layout(self) -> dict:
         """Where every parameter and every optimizer-state segment lives in the flat buffers (they depend on
@@ -179,12 +203,15 @@ class Trainer:
     def state_dict(self):
         self.store.await_all()
         return {"step": self.step, "train_config": self.tc.to_dict(), "model_config": self.cfg.to_dict(),
-                "params": self.store.params, "optimizer": self.opt.state_dict(), "world": self.info.world,
-                "rank": self.info.rank, "dp_mode": self.tc.dp_mode, "layout": self.layout()}
+                "params": self.store.params, "optimizer": self.opt.state_dict(), "world": self.dp_info.world,
+                "rank": self.dp_info.rank, "dp_mode": self.tc.dp_mode, "layout": self.layout(),
+                "tp": self.tp.size, "tp_rank": self.tp.rank}
 
     def load_state_dict(self, sd):
         """Same world size and layout: direct copy. (Other world sizes: ``checkpoint.load`` reshards.)"""
-        if sd["world"] != self.info.world or sd["params"].numel() != self.store.params.numel():
+        if sd.get("tp", 1) != self.tp.size or sd.get("tp_rank", 0) != self.tp.rank:
+            raise ValueError("checkpoint was written with another tensor-parallel layout")
+        if sd["world"] != self.dp_info.world or sd["params"].numel() != self.store.params.numel():
             raise ValueError("checkpoint layout differs from this run's: load it through checkpoint.load")
         self.store.await_all()
         self.store.params.copy_(sd["params"])

@@ -12,7 +12,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 SHAPES = {"llama": (1, 8192, 32, 8, 128), "llama4k": (2, 4096, 32, 8, 128), "guide": (16, 2048, 64, 8, 128),
-          "gpt2": (4, 1024, 12, 12, 64), "s1k": (8, 1024, 32, 8, 128), "s2k": (4, 2048, 32, 8, 128),
+          "gpt2": (4, 1024, 12, 12, 64), "gpt2b": (32, 1024, 12, 12, 64), "s1k": (8, 1024, 32, 8, 128), "s2k": (4, 2048, 32, 8, 128),
           "s512": (16, 512, 32, 8, 128)}
 
 

@@ -62,11 +62,15 @@ def main() -> int:
     ap.add_argument("--tp", type=int, default=1,
                     help="tensor-parallel degree (Llama; TP groups of consecutive ranks, DP across them). The "
                          "headline runs tp 1: Llama-3-8B and its fp32 optimizer state fit one MI355X")
+    ap.add_argument("--layers", type=int, default=0,
+                    help="override the model's layer count (shape rehearsals of big models on one GPU; recorded in "
+                         "the JSON config; never used for the headline)")
     args = ap.parse_args()
 
     import torch
 
     from kubeoperator_amd.parallel.dist import all_reduce_max, barrier, init_distributed, shutdown
+    from kubeoperator_amd.models import get_config
     from kubeoperator_amd.train import SyntheticTokens, TrainConfig, Trainer
 
     info = init_distributed(args.device)
@@ -84,7 +88,8 @@ def main() -> int:
                      overlap_optimizer=bool(args.overlap_opt),
                      transposed_weights=os.environ.get("KOP_TRANSPOSED_W", "1") != "0",
                      cuda_graph=bool(args.cuda_graph), grad_dtype=args.grad_dtype,
-                     wgrad_stream=args.wgrad_stream, recompute=bool(args.recompute), fp8=bool(args.fp8), tp=args.tp)
+                     wgrad_stream=args.wgrad_stream, recompute=bool(args.recompute), fp8=bool(args.fp8), tp=args.tp,
+                     model_overrides={"n_layers": args.layers} if args.layers else {})
     trainer = Trainer(tc, info)
     dp_world = trainer.dp_info.world
     data = SyntheticTokens(trainer.cfg.vocab_size, args.mbs, args.seq, info.device, seed=tc.seed,
@@ -118,9 +123,12 @@ def main() -> int:
     flops_tok = cfg.flops_per_token(args.seq)
     mem_gb = torch.cuda.max_memory_allocated() / 1e9 if cuda else 0.0
     if info.is_main:
-        model_name = {"llama3_8b": "Llama-3-8B", "gpt2_small": "GPT-2-small"}.get(args.model, args.model)
+        model_name = {"llama3_8b": "Llama-3-8B", "gpt2_small": "GPT-2-small",
+                      "llama3_70b": "Llama-3-70B"}.get(args.model, args.model)
+        if args.layers:
+            model_name += f" ({args.layers} of {get_config(args.model).n_layers} layers)"
         out = {
-            "metric": "tokens/sec of bundled Llama-3-8B pod" if args.model == "llama3_8b"
+            "metric": "tokens/sec of bundled Llama-3-8B pod" if args.model == "llama3_8b" and not args.layers
             else f"tokens/sec of bundled {model_name} pod",
             "value": round(value, 2),
             "unit": "tokens/s",

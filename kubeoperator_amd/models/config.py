@@ -63,6 +63,8 @@ class ModelConfig:
 
 CONFIGS = {
     "llama3_8b": ModelConfig("llama3_8b", "llama", 128256, 4096, 32, 32, 8, 14336, 8192, 1e-5, 500000.0),
+    # past one GPU: weights + fp32 AdamW state ~1.1 TB -> tensor parallelism (--tp) inside an 8x MI355X node
+    "llama3_70b": ModelConfig("llama3_70b", "llama", 128256, 8192, 80, 64, 8, 28672, 8192, 1e-5, 500000.0),
     "llama3_1b_proxy": ModelConfig("llama3_1b_proxy", "llama", 128256, 2048, 16, 32, 8, 8192, 8192, 1e-5, 500000.0),
     "gpt2_small": ModelConfig("gpt2_small", "gpt2", 50304, 768, 12, 12, 12, 3072, 1024, 1e-5, 0.0,
                               tie_embeddings=True),

@@ -109,3 +109,22 @@ def test_tensor_parallel_shards_are_a_partition():
         assert torch.equal(got, full.reshape(-1)), name
     with pytest.raises(ValueError, match="divisible"):
         Trainer(_tc(tp=3), DistInfo(world=3))
+
+
+def test_llama3_70b_tp8_shards_fit_one_mi355x():
+    """Llama-3-70B (70.55 B parameters) at tp 8: every rank holds 1/8 of the block projections plus the
+    replicated embeddings / LM head / norms (10.66 B parameters), so weights + gradients + fp32 AdamW state
+    (2 + 2 + 12 bytes per parameter) take ~171 GB of a rank's 288 GB of HBM before activations."""
+    from kubeoperator_amd.models import build_model, get_config
+    from kubeoperator_amd.parallel.tensor import TPContext
+
+    cfg = get_config("llama3_70b")
+    assert abs(cfg.num_params() - 70.55e9) < 0.01e9
+    with torch.device("meta"):
+        full = build_model(cfg)
+        shard = build_model(cfg, TPContext(8, 0, None))
+    blk = lambda m: sum(p.numel() for n, p in m.named_parameters() if n.startswith("layers.") and "norm" not in n)
+    rest = lambda m: sum(p.numel() for n, p in m.named_parameters()) - blk(m)
+    assert blk(shard) * 8 == blk(full) and rest(shard) == rest(full)
+    per_rank = sum(p.numel() for p in shard.parameters())
+    assert 16 * per_rank < 180e9, per_rank

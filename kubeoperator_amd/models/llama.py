@@ -32,7 +32,7 @@ from torch.utils.checkpoint import checkpoint
 from ..ops import functional as kf
 from ..ops.reference import rope_cache
 from ..parallel.flat import ParamSpec
-from ..parallel.tensor import TPContext, check_llama_tp, copy_to_tp, reduce_from_tp
+from ..parallel.tensor import TPContext, check_llama_tp, reduce_from_tp
 from .config import ModelConfig
 
 
@@ -57,11 +57,12 @@ class LlamaBlock(nn.Module):
             y, x1 = kf.rms_norm(x, self.attn_norm, c.norm_eps), x
         else:
             y, x1 = kf.rms_norm(x, self.attn_norm, c.norm_eps, residual=pending)
-        qkv = kf.linear(copy_to_tp(y, tp), self.wqkv)
+        g = tp.group if tp.enabled else None  # column splits: input gradient summed over TP, overlapped
+        qkv = kf.linear(y, self.wqkv, tp_group=g)
         a = kf.rope_attention(qkv, cos, sin, B, S, self.hq, self.hkv, c.head_dim, causal=True)
         a = reduce_from_tp(kf.linear(a, self.wo), tp)
         y2, x2 = kf.rms_norm(x1, self.mlp_norm, c.norm_eps, residual=a)
-        return x2, reduce_from_tp(kf.swiglu_mlp(copy_to_tp(y2, tp), self.w_gate_up, self.w_down), tp)
+        return x2, reduce_from_tp(kf.swiglu_mlp(y2, self.w_gate_up, self.w_down, tp_group=g), tp)
 
 
 class Llama(nn.Module):

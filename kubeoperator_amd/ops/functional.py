@@ -201,10 +201,21 @@ def _bias_grad_into(dy2, out, accumulate):
 # ---------------------------------------------------------------------------------------------------
 # linear
 # ---------------------------------------------------------------------------------------------------
+def _tp_reduce_async(dx, group):
+    """Tensor parallelism, column-split projection: start summing the input gradient over the TP group on
+    RCCL's stream (returns the work, or None) so it overlaps the weight-gradient GEMM that follows."""
+    if group is None or dx is None:
+        return None
+    import torch.distributed as dist
+
+    return dist.all_reduce(dx, group=group, async_op=True)
+
+
 class _Linear(Function):
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, tp_group=None):
         x2 = x.reshape(-1, x.shape[-1])
+        ctx.tp_group = tp_group
         ctx.sx = None
         if b is not None:
             y = torch.addmm(b, x2, w.t())
@@ -225,25 +236,38 @@ class _Linear(Function):
             from . import fp8
 
             dx, dy2, sdy = _dx8(dy2, w)
+            work = _tp_reduce_async(dx, ctx.tp_group)
             dx = dx.view(ctx.in_shape)
             sx = ctx.sx
             dw = _sink(w, lambda out, acc: fp8.wgrad_into(fp8.transpose_cast(dy2, sdy), sdy,
                                                           fp8.transpose_cast(x2, sx), sx, out, acc),
                        dy2, x2, sdy, sx) if ctx.needs_input_grad[1] else None
-            return dx, dw, None
-        dx = _dx(dy2, w).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
+            if work is not None:
+                work.wait()
+            return dx, dw, None, None
+        dx = _dx(dy2, w) if ctx.needs_input_grad[0] else None
+        work = _tp_reduce_async(dx, ctx.tp_group)
+        dx = dx.view(ctx.in_shape) if dx is not None else None
         dw = _sink(w, lambda out, acc: _dw_into(dy2, x2, out, acc), dy2, x2) if ctx.needs_input_grad[1] else None
         db = None
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = _sink(ctx.b, lambda out, acc: _bias_grad_into(dy2, out, acc), dy2)
-        return dx, dw, db
+        if work is not None:
+            work.wait()
+        return dx, dw, db, None
 
 
-def linear(x, w, b=None):
+def linear(x, w, b=None, tp_group=None):
+    """``tp_group``: ``w`` is a column shard of a tensor-parallel projection (``parallel.tensor``) whose input is
+    replicated over the group; the input gradient is summed over it, overlapped with the weight gradient."""
     if not x.is_cuda:
+        if tp_group is not None:
+            from ..parallel.tensor import _CopyToTP
+
+            x = _CopyToTP.apply(x, tp_group)
         return F.linear(x, w, b)
     _gate(w, b)
-    return _Linear.apply(x, w, b)
+    return _Linear.apply(x, w, b, tp_group)
 
 
 # ---------------------------------------------------------------------------------------------------
@@ -408,9 +432,10 @@ class _SwiGLUMLP(Function):
     so neither h nor dgu is transposed separately."""
 
     @staticmethod
-    def forward(ctx, x, w_gu, w_d):
+    def forward(ctx, x, w_gu, w_d, tp_group=None):
         lib = _lib()
         x2 = x.reshape(-1, x.shape[-1])
+        ctx.tp_group = tp_group
         gu, ctx.sx = _fwd8(x2, w_gu)
         T, F2 = gu.shape
         F = F2 // 2
@@ -446,14 +471,18 @@ class _SwiGLUMLP(Function):
             dgu, dgut = lib.swiglu_bwd_t(gu, dh)
         else:
             dgu, dgut = lib.swiglu_bwd(gu, dh), None
-        dx = _dx(dgu, w_gu).view(ctx.in_shape) if ctx.needs_input_grad[0] else None
+        dx = _dx(dgu, w_gu) if ctx.needs_input_grad[0] else None
+        work = _tp_reduce_async(dx, ctx.tp_group)
+        dx = dx.view(ctx.in_shape) if dx is not None else None
         dw_gu = None
         if ctx.needs_input_grad[1]:
             if dgut is not None:
                 dw_gu = _sink(w_gu, lambda out, acc: _mm_into(dgut, transpose(x2).t(), out, acc), dgut, x2)
             else:
                 dw_gu = _sink(w_gu, lambda out, acc: _dw_into(dgu, x2, out, acc), dgu, x2)
-        return dx, dw_gu, dw_d
+        if work is not None:
+            work.wait()
+        return dx, dw_gu, dw_d, None
 
 
     @staticmethod
@@ -472,21 +501,30 @@ class _SwiGLUMLP(Function):
                          dy2, ht, sdy, sh)
         dgu, dgut = lib.swiglu_bwd_t(gu, dh.contiguous())
         dx, dgu, sdgu = _dx8(dgu, w_gu)
+        work = _tp_reduce_async(dx, ctx.tp_group)
         dw_gu = None
         if ctx.needs_input_grad[1]:
             sx = ctx.sx
             dw_gu = _sink(w_gu, lambda out, acc: fp8.wgrad_into(fp8.cast_scaled(dgut, sdgu), sdgu,
                                                                 fp8.transpose_cast(x2, sx), sx, out, acc),
                           dgut, x2, sdgu, sx)
-        return dx.view(ctx.in_shape) if ctx.needs_input_grad[0] else None, dw_gu, dw_d
+        if work is not None:
+            work.wait()
+        return dx.view(ctx.in_shape) if ctx.needs_input_grad[0] else None, dw_gu, dw_d, None
 
 
-def swiglu_mlp(x, w_gu, w_d):
-    """linear(swiglu(linear(x, w_gu)), w_d): the Llama MLP (w_gu = [gate | up] on the output dimension)."""
+def swiglu_mlp(x, w_gu, w_d, tp_group=None):
+    """linear(swiglu(linear(x, w_gu)), w_d): the Llama MLP (w_gu = [gate | up] on the output dimension).
+    ``tp_group``: w_gu / w_d are the FFN-column / FFN-row shards of a tensor-parallel MLP; the input gradient
+    is summed over the group, overlapped with the gate|up weight gradient (the output sum is the caller's)."""
     if not x.is_cuda:
+        if tp_group is not None:
+            from ..parallel.tensor import _CopyToTP
+
+            x = _CopyToTP.apply(x, tp_group)
         return F.linear(swiglu(F.linear(x, w_gu)), w_d)
     _gate(w_gu, w_d)
-    return _SwiGLUMLP.apply(x, w_gu, w_d)
+    return _SwiGLUMLP.apply(x, w_gu, w_d, tp_group)
 
 
 class _GELU(Function):

@@ -18,7 +18,10 @@ Per block (``models.llama.LlamaBlock``), with ``f`` = identity forward / all-red
     y2 = rmsnorm(x + a)                      replicated
     m  = g(swiglu(f(y2) @ Wgu_r^T) @ Wd_r^T) column split of gate|up, row split of Wd
 
-Two all-reduces per block forward and two in backward. Norm weights, embeddings and the LM head are
+Two all-reduces per block forward and two in backward. On the GPU the backward ones are issued
+asynchronously from inside the column-split projections' backward (``ops.functional.linear`` /
+``swiglu_mlp`` with ``tp_group``) right after their data-gradient GEMM, so they run on RCCL's stream under the
+weight-gradient GEMM; the forward ones sit on the critical path. Norm weights, embeddings and the LM head are
 replicated: their gradients come out identical on every TP rank (replicated inputs, all-reduced output
 gradients), so they need no TP reduction; the gradient-norm sum counts each replicated bucket once (it is
 weighted 1/tp before the sum over TP ranks, see ``ops.optim``).

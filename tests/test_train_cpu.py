@@ -395,3 +395,21 @@ def test_elastic_restart_after_injected_rank_failure_resumes_exactly(tmp_path):
         assert torch.equal(a["params"], b["params"]), rank
         for k in ("master", "exp_avg", "exp_avg_sq"):
             assert torch.equal(a["optimizer"][k], b["optimizer"][k]), (rank, k)
+
+
+def test_training_chart_flags_exist_in_the_cli():
+    """Every ``--flag`` the bundled Helm chart's Job passes to ``kubeoperator_amd.train.cli`` is one the CLI parses."""
+    import re
+
+    from kubeoperator_amd.train import cli
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    job = os.path.join(root, "kubeoperator_amd/control/resources/kubeasz/roles/kubeapps/files/charts/pytorch-rocm-train/"
+                             "templates/job.yaml")
+    text = open(job).read()
+    text = text[text.index("kubeoperator_amd.train.cli"):]  # the torchrun launcher's own flags come before
+    flags = set(re.findall(r"^\s*- (--[a-z0-9-]+)", text, re.M))
+    assert {"--model", "--tp", "--recompute", "--fp8"} <= flags
+    src = open(cli.__file__).read()
+    missing = [f for f in flags if f'"{f}"' not in src]
+    assert not missing, missing

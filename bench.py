@@ -59,6 +59,8 @@ def main() -> int:
     ap.add_argument("--cuda-graph", type=int, default=0, choices=[0, 1],
                     help="replay each micro-batch's forward + backward as a captured HIP graph (one GPU only; pays "
                          "off when small micro-batches are bound by host-side launch overhead)")
+    ap.add_argument("--sp", type=int, default=0, choices=[0, 1],
+                    help="sequence parallelism with --tp > 1: norms, residual stream and LM head on 1/tp of the rows")
     ap.add_argument("--tp", type=int, default=1,
                     help="tensor-parallel degree (Llama; TP groups of consecutive ranks, DP across them). The "
                          "headline runs tp 1: Llama-3-8B and its fp32 optimizer state fit one MI355X")
@@ -88,7 +90,7 @@ def main() -> int:
                      overlap_optimizer=bool(args.overlap_opt),
                      transposed_weights=os.environ.get("KOP_TRANSPOSED_W", "1") != "0",
                      cuda_graph=bool(args.cuda_graph), grad_dtype=args.grad_dtype,
-                     wgrad_stream=args.wgrad_stream, recompute=bool(args.recompute), fp8=bool(args.fp8), tp=args.tp,
+                     wgrad_stream=args.wgrad_stream, recompute=bool(args.recompute), fp8=bool(args.fp8), tp=args.tp, sp=bool(args.sp),
                      model_overrides={"n_layers": args.layers} if args.layers else {})
     trainer = Trainer(tc, info)
     dp_world = trainer.dp_info.world
@@ -148,7 +150,8 @@ def main() -> int:
                 "micro_batch_per_gpu": args.mbs,
                 "grad_accum": args.accum,
                 "seq_len": args.seq,
-                "parallelism": (f"tp{args.tp}-" if args.tp > 1 else "") + f"dp{dp_world}"
+                "parallelism": (f"tp{args.tp}-" if args.tp > 1 else "") + ("sp-" if args.sp and args.tp > 1 else "")
+                + f"dp{dp_world}"
                 + ("-zero1" if args.dp == "zero1" and dp_world > 1 else ""),
                 "optimizer": "fused AdamW (fp32 master/moments), grad clip 1.0",
                 "optimizer_overlap": bool(args.overlap_opt),

@@ -32,7 +32,7 @@ from torch.utils.checkpoint import checkpoint
 from ..ops import functional as kf
 from ..ops.reference import rope_cache
 from ..parallel.flat import ParamSpec
-from ..parallel.tensor import TPContext, check_llama_tp, reduce_from_tp
+from ..parallel.tensor import TPContext, check_llama_tp, reduce_from_tp, sp_gather, sp_rows, sp_scatter
 from .config import ModelConfig
 
 
@@ -57,6 +57,11 @@ class LlamaBlock(nn.Module):
             y, x1 = kf.rms_norm(x, self.attn_norm, c.norm_eps), x
         else:
             y, x1 = kf.rms_norm(x, self.attn_norm, c.norm_eps, residual=pending)
+        if tp.seq_parallel:  # token-row shards: gathered into the column splits, reduce-scattered out of the rows
+            qkv = kf.linear(sp_gather(y, tp), self.wqkv)
+            a = kf.rope_attention(qkv, cos, sin, B, S, self.hq, self.hkv, c.head_dim, causal=True)
+            y2, x2 = kf.rms_norm(x1, self.mlp_norm, c.norm_eps, residual=sp_scatter(kf.linear(a, self.wo), tp))
+            return x2, sp_scatter(kf.swiglu_mlp(sp_gather(y2, tp), self.w_gate_up, self.w_down), tp)
         g = tp.group if tp.enabled else None  # column splits: input gradient summed over TP, overlapped
         qkv = kf.linear(y, self.wqkv, tp_group=g)
         a = kf.rope_attention(qkv, cos, sin, B, S, self.hq, self.hkv, c.head_dim, causal=True)
@@ -117,7 +122,11 @@ class Llama(nn.Module):
     def forward(self, ids: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
         B, S = ids.shape
         cos, sin = self.rope_tables(S, ids.device)
-        x = kf.embedding(ids.reshape(-1), self.tok_emb)
+        ids, targets = ids.reshape(-1), targets.reshape(-1)
+        if self.tp.seq_parallel:  # this rank's token rows: embedding, norms, LM head and loss on 1/tp of them
+            rows = sp_rows(ids.numel(), self.tp)
+            ids, targets = ids[rows], targets[rows]
+        x = kf.embedding(ids, self.tok_emb)
         pending = None
         for blk in self.layers:
             if self.recompute and torch.is_grad_enabled():
@@ -127,4 +136,4 @@ class Llama(nn.Module):
                 x, pending = blk(x, pending, cos, sin, B, S)
         y, _ = kf.rms_norm(x, self.final_norm, self.cfg.norm_eps, residual=pending)
         head = self.tok_emb if self.cfg.tie_embeddings else self.lm_head
-        return kf.cross_entropy_lmhead(y, head, targets.reshape(-1))
+        return kf.cross_entropy_lmhead(y, head, targets)

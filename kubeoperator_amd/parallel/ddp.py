@@ -40,6 +40,11 @@ class DataParallel:
         self.info = info
         self.group = info.group
         self.tp = tp
+        # sequence parallelism: replicated parameters saw only this rank's token rows, so their buckets are
+        # reduced over the whole job (TP x DP ranks), the sharded ones over the DP group
+        self.sp = tp is not None and tp.seq_parallel
+        self.job_rank = info.global_rank if info.global_rank >= 0 else info.rank
+        self.job_world = info.world * (tp.size if tp is not None else 1)
         self.mode = mode
         self.world = info.world
         self.rank = info.rank
@@ -50,21 +55,28 @@ class DataParallel:
         store.on_ready = self._on_ready
         self.overlapped = False  # set once the optimizer publishes ZeRO-1 gathers itself
 
+    def _topo(self, b: Bucket):
+        """(group, rank, world) the bucket's gradient collective and ZeRO-1 pieces run over."""
+        if self.sp and not b.shard:
+            return None, self.job_rank, self.job_world
+        return self.group, self.rank, self.world
+
     # -------------------------------------------------------------------------------------------
     def broadcast_params(self) -> None:
         if self.world > 1:
             dist.broadcast(self.store.params, src=self.info.src, group=self.group)
 
     def _on_ready(self, b: Bucket) -> None:
-        if self.world == 1 or not self.sync:
+        group, rank, world = self._topo(b)
+        if world == 1 or not self.sync:
             return
         g = self.store.grads[b.start:b.end]
         self.comm_bytes += g.numel() * g.element_size()
         if self.mode == "allreduce":
-            self._works.append(dist.all_reduce(g, group=self.group, async_op=True))
+            self._works.append(dist.all_reduce(g, group=group, async_op=True))
         else:
-            a, e = b.piece(self.rank, self.world)
-            self._works.append(dist.reduce_scatter_tensor(self.store.grads[a:e], g, group=self.group, async_op=True))
+            a, e = b.piece(rank, world)
+            self._works.append(dist.reduce_scatter_tensor(self.store.grads[a:e], g, group=group, async_op=True))
 
     def finish_grads(self) -> None:
         """Make the current (compute) stream wait for every outstanding gradient collective."""
@@ -74,30 +86,38 @@ class DataParallel:
 
     @property
     def grad_scale(self) -> float:
-        return 1.0 / self.world
+        # under SP every rank's loss is the mean over its 1/tp of the rows: the summed gradients are tp x the job's
+        return 1.0 / (self.world * (self.tp.size if self.sp else 1))
 
     def optimizer_segments(self) -> list[Segment]:
         st = self.store
         wd_of = {True: None, False: 0.0}
-        rep_w = 1.0 / self.tp.size if self.tp is not None and self.tp.enabled else 1.0
+        tp = self.tp is not None and self.tp.enabled
         segs = []
         for b in st.buckets:
-            a, e = (b.start, b.end) if self.mode == "allreduce" or self.world == 1 else b.piece(self.rank, self.world)
+            _, rank, world = self._topo(b)
+            whole = self.mode == "allreduce" or world == 1
+            a, e = (b.start, b.end) if whole else b.piece(rank, world)
+            # a replicated bucket's piece held identically by every TP rank counts 1/tp in the grad norm
+            dup = tp and not b.shard and (whole or not self.sp)
             segs.append(Segment(st.params[a:e], st.grads[a:e], wd_of[b.decay], b.index,
-                                1.0 if b.shard else rep_w))
+                                1.0 / self.tp.size if dup else 1.0))
         return segs
 
     def publish_segment(self, seg: Segment):
         """Optimizer-overlap hook, called on the optimizer stream right after a bucket's AdamW launch.
         ZeRO-1: start the bucket's in-place all-gather there and hand its work back as the bucket's gate."""
-        if self.mode != "zero1" or self.world == 1:
+        if self.mode != "zero1":
+            return None
+        b = self.store.buckets[seg.bucket]
+        group, rank, world = self._topo(b)
+        if world == 1:
             return None
         self.overlapped = True
-        b = self.store.buckets[seg.bucket]
-        a, e = b.piece(self.rank, self.world)
-        return self._gather(b, a, e, async_op=True)
+        a, e = b.piece(rank, world)
+        return self._gather(b, a, e, group, async_op=True)
 
-    def _gather(self, b: Bucket, a: int, e: int, async_op: bool):
+    def _gather(self, b: Bucket, a: int, e: int, group, async_op: bool):
         """In-place all-gather of the bucket's updated pieces (RCCL on GPU; gloo runs the same call on CPU).
 
         Through ``params.data``: the parameters are views of the flat buffer and share ITS autograd version
@@ -106,13 +126,13 @@ class DataParallel:
         ``copy_`` at ``wait()``, i.e. mid-forward when the gate is resolved). The ordering that matters --
         bucket Y written before any kernel reads it -- is the gate's stream dependency, not autograd's."""
         pd = self.store.params.data
-        return dist.all_gather_into_tensor(pd[b.start:b.end], pd[a:e], group=self.group, async_op=async_op)
+        return dist.all_gather_into_tensor(pd[b.start:b.end], pd[a:e], group=group, async_op=async_op)
 
     def norm_allreduce(self):
         """The grad-norm sum of squares is summed over the ranks holding distinct gradient pieces: the DP
         group under ZeRO-1, the TP group under tensor parallelism, the whole job with both."""
         tp = self.tp is not None and self.tp.enabled
-        if self.mode == "zero1" and self.world > 1:
+        if self.mode == "zero1" and (self.world > 1 or self.sp):
             if tp:
                 return lambda t: dist.all_reduce(t)  # every rank: DP pieces x TP shards
             return lambda t: dist.all_reduce(t, group=self.group)
@@ -122,12 +142,15 @@ class DataParallel:
 
     def after_step(self) -> None:
         """ZeRO-1: all-gather the updated bf16 parameter pieces back into every rank's flat buffer."""
-        if self.mode != "zero1" or self.world == 1 or self.overlapped:
+        if self.mode != "zero1" or self.overlapped:
             return
         st = self.store
         for b in st.buckets:
-            a, e = b.piece(self.rank, self.world)
-            w = self._gather(b, a, e, async_op=True)
+            group, rank, world = self._topo(b)
+            if world == 1:
+                continue
+            a, e = b.piece(rank, world)
+            w = self._gather(b, a, e, group, async_op=True)
             if w is not None:
                 self._gather_works.append(w)
         self.wait_params()

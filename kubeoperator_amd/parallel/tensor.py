@@ -26,6 +26,14 @@ replicated: their gradients come out identical on every TP rank (replicated inpu
 gradients), so they need no TP reduction; the gradient-norm sum counts each replicated bucket once (it is
 weighted 1/tp before the sum over TP ranks, see ``ops.optim``).
 
+Sequence parallelism (``--sp``, Megatron-SP): between the projections the residual stream, the norms and the
+LM head + cross-entropy work on 1/tp of the token rows. ``f`` becomes an all-gather of the rows (reduce-scatter
+in backward) and ``g`` a reduce-scatter (all-gather in backward): the same bytes on xGMI as the two all-reduces,
+while norm / residual activations and the LM head's vocabulary GEMMs and cross-entropy shrink by tp (without SP
+every TP rank computes the whole 128k-vocabulary head). Each rank's loss is the mean over its rows, so all
+gradients come out tp x the job's; replicated parameters (norms, embeddings, LM head) then see only their rank's
+rows and are reduced over the whole job (TP x DP) instead of the DP group (``parallel.ddp``).
+
 The reference has no model code at all (TP "not required; optional later"); this is the
 MI355X-native option for models past Llama-3-8B.
 """
@@ -45,13 +53,18 @@ class TPContext:
     size: int = 1
     rank: int = 0
     group: object = None  # torch.distributed group of this rank's TP peers (None when size == 1)
+    sp: bool = False  # sequence parallelism: the residual stream is split over the group by token rows
 
     @property
     def enabled(self) -> bool:
         return self.size > 1
 
+    @property
+    def seq_parallel(self) -> bool:
+        return self.sp and self.size > 1
 
-def make_groups(info: DistInfo, tp: int) -> tuple[DistInfo, TPContext]:
+
+def make_groups(info: DistInfo, tp: int, sp: bool = False) -> tuple[DistInfo, TPContext]:
     """Split the job into TP groups of ``tp`` consecutive ranks and DP groups across them. Returns the
     data-parallel view of this rank (``DistInfo`` with the DP rank / size / group) and its TP context.
     Every rank creates every group, in the same order (``new_group`` is collective)."""
@@ -74,7 +87,7 @@ def make_groups(info: DistInfo, tp: int) -> tuple[DistInfo, TPContext]:
             dp_group, dp_ranks = grp, ranks
     dp_info = DistInfo(rank=info.rank // tp, local_rank=info.local_rank, world=world // tp, backend=info.backend,
                        device=info.device, group=dp_group, src=dp_ranks[0], global_rank=info.rank)
-    return dp_info, TPContext(tp, info.rank % tp, tp_group)
+    return dp_info, TPContext(tp, info.rank % tp, tp_group, sp)
 
 
 class _CopyToTP(Function):
@@ -105,6 +118,62 @@ class _ReduceFromTP(Function):
     @staticmethod
     def backward(ctx, g):
         return g, None
+
+
+class _GatherFromSP(Function):
+    """Sequence parallelism, entering a column split: the token-row shards of the group are concatenated
+    (all-gather along rows) in forward; the full-row gradient is reduce-scattered back to the shards."""
+
+    @staticmethod
+    def forward(ctx, x, group, n):
+        ctx.group, ctx.n = group, n
+        x = x.contiguous()
+        out = torch.empty((x.shape[0] * n,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        dist.all_gather_into_tensor(out, x, group=group)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        out = torch.empty((g.shape[0] // ctx.n,) + tuple(g.shape[1:]), dtype=g.dtype, device=g.device)
+        dist.reduce_scatter_tensor(out, g, group=ctx.group)
+        return out, None, None
+
+
+class _ScatterToSP(Function):
+    """Sequence parallelism, leaving a row split: the partial full-row outputs are summed AND split by token
+    rows (reduce-scatter) in forward; the shard gradients are all-gathered in backward."""
+
+    @staticmethod
+    def forward(ctx, x, group, n):
+        ctx.group, ctx.n = group, n
+        x = x.contiguous()
+        out = torch.empty((x.shape[0] // n,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        dist.reduce_scatter_tensor(out, x, group=group)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        out = torch.empty((g.shape[0] * ctx.n,) + tuple(g.shape[1:]), dtype=g.dtype, device=g.device)
+        dist.all_gather_into_tensor(out, g, group=ctx.group)
+        return out, None, None
+
+
+def sp_gather(x: torch.Tensor, tp: TPContext) -> torch.Tensor:
+    return _GatherFromSP.apply(x, tp.group, tp.size)
+
+
+def sp_scatter(x: torch.Tensor, tp: TPContext) -> torch.Tensor:
+    return _ScatterToSP.apply(x, tp.group, tp.size)
+
+
+def sp_rows(n_rows: int, tp: TPContext) -> slice:
+    """This rank's token rows of a [n_rows, ...] activation under sequence parallelism."""
+    if n_rows % tp.size != 0:
+        raise ValueError(f"{n_rows} token rows do not split over tp {tp.size} (sequence parallelism)")
+    k = n_rows // tp.size
+    return slice(tp.rank * k, (tp.rank + 1) * k)
 
 
 def copy_to_tp(x: torch.Tensor, tp: TPContext) -> torch.Tensor:

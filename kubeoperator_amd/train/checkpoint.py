@@ -88,6 +88,8 @@ def load(trainer, directory: str, info: DistInfo, step: int | None = None) -> in
     files = _files(d)
     own = os.path.join(d, f"rank_{info.rank}.pt")
     head = torch.load(files[0], map_location="cpu", weights_only=True, mmap=True)
+    if getattr(getattr(trainer, "tp", None), "seq_parallel", False) and head["world"] != info.world:
+        raise ValueError("a sequence-parallel checkpoint resumes on the topology that wrote it")
     if "layout" in head:  # identical flat layout (world size AND bucket boundaries): plain copy
         lay = trainer.layout()
         same = (head["world"] == info.world and head["layout"]["offsets"] == lay["offsets"]

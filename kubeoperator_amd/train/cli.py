@@ -47,6 +47,8 @@ def main(argv=None) -> int:
                     help="gradient buffer precision (fp32: accumulation and DP reduction in fp32)")
     ap.add_argument("--cuda-graph", type=int, default=0, choices=[0, 1],
                     help="replay micro-batches as captured HIP graphs (one GPU; small micro-batches)")
+    ap.add_argument("--sp", type=int, default=0, choices=[0, 1],
+                    help="sequence parallelism with --tp > 1: norms, residual stream and LM head on 1/tp of the rows")
     ap.add_argument("--tp", type=int, default=1,
                     help="tensor-parallel degree (Llama): TP groups of consecutive ranks, data parallelism across them")
     ap.add_argument("--metrics-port", type=int, default=0, help="rank 0 serves Prometheus metrics here (0: off)")
@@ -76,7 +78,7 @@ def main(argv=None) -> int:
     tc = TrainConfig(model=a.model, micro_batch=a.mbs, seq_len=a.seq, grad_accum=a.accum, lr=a.lr,
                      warmup_steps=a.warmup, total_steps=a.steps, dp_mode=a.dp, bucket_mb=a.bucket_mb, overlap_optimizer=bool(a.overlap_opt),
                      cuda_graph=bool(a.cuda_graph), grad_dtype=a.grad_dtype,
-                     wgrad_stream=a.wgrad_stream, recompute=bool(a.recompute), fp8=bool(a.fp8), tp=a.tp)
+                     wgrad_stream=a.wgrad_stream, recompute=bool(a.recompute), fp8=bool(a.fp8), tp=a.tp, sp=bool(a.sp))
     tr = Trainer(tc, info)
     dpi = tr.dp_info  # the TP ranks of a group read the same tokens
     if a.resume and a.ckpt_dir:

@@ -45,6 +45,7 @@ class TrainConfig:
     recompute: bool = False  # per-block activation recompute (long sequences: only block inputs stay saved)
     wgrad_stream: str = "auto"  # weight-gradient GEMMs on a side stream: auto (narrow models, hidden < 2048) | on | off
     tp: int = 1  # tensor-parallel degree (Llama; TP groups of consecutive ranks, DP across them: parallel.tensor)
+    sp: bool = False  # sequence parallelism on top of TP (norms, residual stream, LM head on 1/tp of the rows)
     seed: int = 1234
     model_overrides: dict = field(default_factory=dict)
 
@@ -65,7 +66,7 @@ class Trainer:
         self.info = info
         # data-parallel view of this rank + its tensor-parallel group (the whole job and no TP when tp == 1)
         check_llama_tp(get_config(tc.model, **tc.model_overrides), tc.tp)
-        self.dp_info, self.tp = make_groups(info, tc.tp)
+        self.dp_info, self.tp = make_groups(info, tc.tp, tc.sp)
         overrides = dict(tc.model_overrides)
         base = get_config(tc.model)
         if tc.seq_len > base.max_seq_len and base.arch == "llama" and "max_seq_len" not in overrides:
@@ -81,7 +82,9 @@ class Trainer:
         self.model.recompute = bool(tc.recompute)
         if tc.grad_dtype not in ("bf16", "fp32"):
             raise ValueError(f"grad_dtype must be bf16 or fp32, not {tc.grad_dtype!r}")
-        self.store = FlatParamStore(self.model, self.model.param_specs(), dev, world=self.dp_info.world,
+        # SP reduces replicated buckets over the whole job: their ZeRO-1 pieces split over every rank
+        self.store = FlatParamStore(self.model, self.model.param_specs(), dev,
+                                    world=info.world if self.tp.seq_parallel else self.dp_info.world,
                                     bucket_bytes=tc.bucket_mb * 1024 * 1024,
                                     grad_dtype=torch.float32 if tc.grad_dtype == "fp32" else torch.bfloat16)
         self.store.init_weights(seed=tc.seed, shard_rank=self.tp.rank)
@@ -150,7 +153,13 @@ class Trainer:
             self.store.refresh_transposed()
             self.store.refresh_fp8()
         self.step += 1
-        return torch.stack(losses).mean()
+        loss = torch.stack(losses).mean()
+        if self.tp.seq_parallel:  # each TP rank's loss covers its 1/tp of the rows
+            import torch.distributed as dist
+
+            dist.all_reduce(loss, group=self.tp.group)
+            loss = loss / self.tp.size
+        return loss
 
     # HIP graphs -----------------------------------------------------------------------------------
     def _replay(self, key: int, ids, tgt) -> torch.Tensor:

@@ -31,13 +31,13 @@ def _full_init():
     return {n: p.detach().clone() for n, p in ref.store.named_params()}
 
 
-def _worker(rank, world, tp, init, mode, steps, out_q):
+def _worker(rank, world, tp, init, mode, steps, out_q, sp=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       KOP_DIST_INIT=init)
     torch.set_num_threads(1)
     from kubeoperator_amd.parallel.dist import init_distributed, shutdown
     info = init_distributed("cpu")
-    tr = Trainer(_tc(tp=tp, dp_mode=mode), info)
+    tr = Trainer(_tc(tp=tp, dp_mode=mode, sp=sp), info)
     tr.load_full_weights(_full_init())
     dp, dpr = tr.dp_info.world, tr.dp_info.rank
     losses = []
@@ -49,11 +49,11 @@ def _worker(rank, world, tp, init, mode, steps, out_q):
     shutdown(info)
 
 
-def _run(world, tp, mode, tmp_path, steps=3):
+def _run(world, tp, mode, tmp_path, steps=3, sp=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    init = f"file://{tmp_path}/rdzv-{world}-{tp}"
-    procs = [ctx.Process(target=_worker, args=(r, world, tp, init, mode, steps, q)) for r in range(world)]
+    init = f"file://{tmp_path}/rdzv-{world}-{tp}-{int(sp)}"
+    procs = [ctx.Process(target=_worker, args=(r, world, tp, init, mode, steps, q, sp)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -66,9 +66,11 @@ def _run(world, tp, mode, tmp_path, steps=3):
     return res
 
 
-@pytest.mark.parametrize("world,tp,mode", [(2, 2, "allreduce"), (4, 2, "zero1")])
-def test_tensor_parallel_matches_single_process(world, tp, mode, tmp_path):
-    res = _run(world, tp, mode, tmp_path)
+@pytest.mark.parametrize("world,tp,mode,sp", [(2, 2, "allreduce", False), (4, 2, "zero1", False),
+                                              (2, 2, "zero1", True), (4, 2, "zero1", True), (4, 2, "allreduce", True)])
+def test_tensor_parallel_matches_single_process(world, tp, mode, sp, tmp_path):
+    """sp: sequence parallelism on top (norms / residual stream / LM head on 1/tp of the token rows)."""
+    res = _run(world, tp, mode, tmp_path, sp=sp)
     dp = world // tp
     single = Trainer(_tc(micro_batch=2 * dp), DistInfo())
     single.load_full_weights(_full_init())

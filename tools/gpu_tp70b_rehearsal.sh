@@ -7,6 +7,6 @@ set -o pipefail
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 KOP_DIST_BACKEND=gloo KOP_DEVICE_INDEX=0 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-  --master-addr 127.0.0.1 --master-port 29695 bench.py --gpus 2 --tp 2 --model llama3_70b --layers 4 --recompute 1 \
+  --master-addr 127.0.0.1 --master-port 29695 bench.py --gpus 2 --tp 2 --model llama3_70b --layers 4 --recompute 1 --sp 1 \
   --seq 8192 --mbs 1 --accum 1 --steps 2 --warmup 1 --gemm-tuning off > gpurun_out/tp70b.log 2>&1
 rc=$?; echo "70b tp2 rc=$rc"; grep metric gpurun_out/tp70b.log | cut -c1-900; tail -3 gpurun_out/tp70b.log | cut -c1-300; exit $rc

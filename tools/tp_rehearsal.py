@@ -28,6 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tp", type=int, default=2)
     ap.add_argument("--mode", default="zero1", choices=["zero1", "allreduce"])
+    ap.add_argument("--sp", type=int, default=0, choices=[0, 1], help="sequence parallelism on top of TP")
     ap.add_argument("--model", default="tiny_llama")
     ap.add_argument("--seq", type=int, default=256)
     ap.add_argument("--mbs", type=int, default=2)
@@ -44,7 +45,7 @@ def main():
     kw = dict(model=a.model, seq_len=a.seq, warmup_steps=1, total_steps=10, bucket_mb=1, lr=1e-1, eps=1.0)
     one_info = DistInfo(0, 0, 1, "none", info.device)
     full = {n: p.detach().clone() for n, p in Trainer(TrainConfig(**kw), one_info).store.named_params()}
-    tr = Trainer(TrainConfig(micro_batch=a.mbs, dp_mode=a.mode, tp=a.tp, **kw), info)
+    tr = Trainer(TrainConfig(micro_batch=a.mbs, dp_mode=a.mode, tp=a.tp, sp=bool(a.sp), **kw), info)
     tr.load_full_weights(full)
     dp, dpr = tr.dp_info.world, tr.dp_info.rank
     sl = slice(a.mbs * dpr, a.mbs * (dpr + 1))
@@ -79,7 +80,7 @@ def main():
             den += float((w - w0).pow(2).sum())
     rel = (num / max(den, 1e-30)) ** 0.5
     ok = rel < 0.05
-    print(json.dumps({"rehearsal": f"tp{a.tp}-dp{dp}-{a.mode}", "model": a.model, "rel_update_error": rel,
+    print(json.dumps({"rehearsal": f"tp{a.tp}-" + ("sp-" if a.sp else "") + f"dp{dp}-{a.mode}", "model": a.model, "rel_update_error": rel,
                       "ok": ok, "buckets": len(tr.store.buckets), "optimizer_overlap": tr.opt.overlap}), flush=True)
     return 0 if ok else 1
 

@@ -337,6 +337,36 @@ void flash_attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Ten
 
 }  // namespace
 
+// ------------------------------------------------------------------ decode attention (serving)
+// q: [B, Hq*D] rows (strided view allowed); k_cache / v_cache: [B, Smax, Hkv, D] contiguous; lens: [B] int32
+// (valid keys per sequence, 1 <= lens <= Smax); max_len bounds lens (host value: sizes the split grid)
+Tensor decode_attn(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& lens, int64_t max_len,
+                   double scale) {
+  check_bf16(q, "q");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  check_rows(q, "q");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.is_contiguous() && v_cache.is_contiguous() &&
+                  k_cache.sizes() == v_cache.sizes(), "caches must be contiguous [B, Smax, Hkv, D] and equal");
+  check_aligned(k_cache, "k_cache");
+  check_aligned(v_cache, "v_cache");
+  TORCH_CHECK(lens.is_cuda() && lens.scalar_type() == at::kInt && lens.is_contiguous(), "lens must be int32 on the GPU");
+  const int B = (int)k_cache.size(0), Smax = (int)k_cache.size(1), Hkv = (int)k_cache.size(2), D = (int)k_cache.size(3);
+  TORCH_CHECK(q.size(0) == B && lens.numel() == B, "batch mismatch");
+  TORCH_CHECK(q.size(1) % D == 0, "q width must be a multiple of head_dim");
+  const int Hq = (int)(q.size(1) / D);
+  TORCH_CHECK(max_len >= 1 && max_len <= Smax, "max_len must be in [1, Smax]");
+  const int nsplit = kop::decode_attn_splits((int)max_len);
+  auto o = at::empty({B, (int64_t)Hq * D}, q.options());
+  auto part_o = at::empty({(int64_t)B * Hq * nsplit * D}, q.options().dtype(at::kFloat));
+  auto part_ml = at::empty({(int64_t)B * Hq * nsplit * 2}, q.options().dtype(at::kFloat));
+  rc(kop::decode_attn(bp(q), q.stride(0), bp(k_cache), bp(v_cache), lens.data_ptr<int>(), bp(o), o.stride(0),
+                      part_o.data_ptr<float>(), part_ml.data_ptr<float>(), B, Smax, Hq, Hkv, D, nsplit, (float)scale,
+                      cur_stream()),
+     "decode_attn");
+  return o;
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "kubeoperator_amd gfx950 (MI355X) HIP kernels";
   m.attr("ARCH") = "gfx950";
@@ -360,6 +390,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_sumsq_", &grad_sumsq_);
   m.def("clip_coef_", &clip_coef_);
   m.def("flash_attn_fwd", &flash_attn_fwd);
+  m.def("decode_attn", &decode_attn);
   m.def("flash_attn_bwd_workspace", &flash_attn_bwd_workspace);
   m.def("flash_attn_bwd", &flash_attn_bwd);
   m.def("flash_attn_set_dq_variant", [](int64_t v) { return (int64_t)kop::flash_attn_set_dq_variant((int)v); });

@@ -1,0 +1,250 @@
+// Decode attention for gfx950 (serving): one new query token per sequence against its KV cache, GQA, split-K
+// ("flash decoding") so a batch of a few sequences still fills the 256 CUs.
+//
+//   q      [B, Hq * D]           bf16 rows (row stride qs: the Q columns of the fused QKV projection)
+//   cache  K, V [B, Smax, Hkv, D] bf16, keys [0, len[b]) valid
+//   o      [B, Hq * D]           bf16
+//
+// Memory-bound: every step streams the whole live cache (Llama-3-8B, 8k context: 4 MiB of K+V per sequence
+// and layer), so the kernel is built around coalesced 16-byte loads and reuse of each K/V row by all
+// G = Hq / Hkv query heads of its group, not around matrix cores (M = G <= 8 query rows per key tile would
+// leave MFMA 32-row tiles mostly empty).
+//
+// Pass 1: grid (splits, B * Hkv), 256 threads. A workgroup owns CH = 256 keys of one (sequence, KV head).
+//   thread t = (key group kg = t / 16, segment sg = t % 16): the 16 threads of a key group read one 256-byte
+//   K row (D = 128) as 16 x 16 B -- a wave loads 4 whole rows per instruction -- and each keeps G partial dot
+//   products of its 8 dims, summed over the 16 lanes with 4 butterfly shuffles. Scores (already scaled by
+//   log2 e / sqrt(D)) go to LDS; the workgroup's max / sum of exp2 per head come from a block reduction;
+//   P . V runs with the same (key group, segment) mapping on the V rows (every K and V load of a thread is
+//   issued up front); the key groups' [G x D] partial sums are added with butterflies inside each wave, then
+//   over the 4 waves in LDS. Output per split: unnormalised acc [G, D], running max m and sum l (fp32).
+// Pass 2: grid B * Hq, D / 2 threads: o = sum_s acc_s 2^(m_s - M) / sum_s l_s 2^(m_s - M).
+#include "common.h"
+#include "kernels.h"
+
+namespace kop {
+
+namespace {
+constexpr int kCH = 256;          // keys per workgroup (one split)
+constexpr int kThreads = 256;
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kNegBig = -1e30f;
+}  // namespace
+
+template <int D, int G>
+__global__ void __launch_bounds__(kThreads) decode_attn_split_kernel(
+    const bf16_t* __restrict__ q, int64_t qs, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+    const int* __restrict__ lens, int Smax, int Hkv, float scale_log2, float* __restrict__ part_o,
+    float* __restrict__ part_ml, int nsplit) {
+  constexpr int SEGS = D / 8;         // 16-byte segments per row (16 at D = 128, 8 at D = 64)
+  constexpr int KG = kThreads / SEGS; // key groups (16 / 32)
+  constexpr int KPT = kCH / KG;       // keys per thread (16 / 8)
+  __shared__ float s_p[G][kCH];       // scores, then probabilities
+  __shared__ float s_red[G][kThreads / 64];
+  __shared__ f32x4 s_acc[kThreads / 64][G][D / 4];
+  const int split = blockIdx.x;
+  const int b = blockIdx.y / Hkv, kvh = blockIdx.y % Hkv;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int kg = t / SEGS, sg = t % SEGS;
+  const int len = lens[b];
+  const int k0 = split * kCH;
+  const int64_t rs = (int64_t)Hkv * D;  // cache row stride (elements) between consecutive keys
+  const bf16_t* kbase = kc + ((int64_t)b * Smax) * rs + (int64_t)kvh * D + sg * 8;
+  const bf16_t* vbase = vc + ((int64_t)b * Smax) * rs + (int64_t)kvh * D + sg * 8;
+  float* po = part_o + (((int64_t)b * Hkv + kvh) * G * nsplit) * D;  // [G][nsplit][D] for this (b, kvh)
+  float* pml = part_ml + (((int64_t)b * Hkv + kvh) * G * nsplit) * 2;
+  if (k0 >= len) {  // split past the sequence: an empty partial
+    if (t < G) {
+      pml[(t * nsplit + split) * 2] = kNegBig;
+      pml[(t * nsplit + split) * 2 + 1] = 0.f;
+    }
+    for (int i = t; i < G * D; i += kThreads) po[((i / D) * nsplit + split) * D + i % D] = 0.f;
+    return;
+  }
+  // this thread's 8 query dims of each head of the group, pre-scaled
+  float qv[G][8];
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    unpack8(*reinterpret_cast<const u32x4*>(q + (int64_t)b * qs + (int64_t)(kvh * G + h) * D + sg * 8), qv[h]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) qv[h][i] *= scale_log2;
+  }
+  // ---- every K and V row segment of this thread in flight at once (V is consumed after the softmax)
+  u32x4 kr[KPT], vr[KPT];
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    const int key = k0 + kg + KG * j;
+    kr[j] = key < len ? *reinterpret_cast<const u32x4*>(kbase + (int64_t)key * rs) : u32x4{0u, 0u, 0u, 0u};
+  }
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    const int key = k0 + kg + KG * j;
+    vr[j] = key < len ? *reinterpret_cast<const u32x4*>(vbase + (int64_t)key * rs) : u32x4{0u, 0u, 0u, 0u};
+  }
+  // ---- scores: key k0 + kg + KG * j
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    float kf[8];
+    unpack8(kr[j], kf);
+    float d[G];
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+      float a = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a += qv[h][i] * kf[i];
+      d[h] = a;
+    }
+#pragma unroll
+    for (int o = SEGS / 2; o > 0; o >>= 1)
+#pragma unroll
+      for (int h = 0; h < G; ++h) d[h] += __shfl_xor(d[h], o, 64);
+    const int kl = kg + KG * j;
+    if (sg < G) {  // lane sg of the key group stores head sg's score (all lanes hold every head's sum)
+      float v = 0.f;
+#pragma unroll
+      for (int h = 0; h < G; ++h) v = (h == sg) ? d[h] : v;
+      s_p[sg][kl] = (k0 + kl < len) ? v : kNegBig;
+    }
+  }
+  __syncthreads();
+  // ---- per-head max and sum over the CH keys (thread t covers key t of every head)
+  float m[G], l[G];
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    const float mv = wave_max(s_p[h][t]);
+    if (lane == 0) s_red[h][wv] = mv;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    float mm = s_red[h][0];
+#pragma unroll
+    for (int w = 1; w < kThreads / 64; ++w) mm = fmaxf(mm, s_red[h][w]);
+    m[h] = mm;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    const float s = s_p[h][t];
+    const float p = s <= 0.5f * kNegBig ? 0.f : exp2f(s - m[h]);
+    s_p[h][t] = p;
+    const float sv = wave_sum(p);
+    if (lane == 0) s_red[h][wv] = sv;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < G; ++h) {
+    float ss = 0.f;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; ++w) ss += s_red[h][w];
+    l[h] = ss;
+  }
+  // ---- P . V with the score mapping: this thread's 8 dims of keys kg + KG * j
+  float acc[G][8];
+#pragma unroll
+  for (int h = 0; h < G; ++h)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[h][i] = 0.f;
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    float vf[8];
+    unpack8(vr[j], vf);
+    const int kl = kg + KG * j;
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+      const float p = s_p[h][kl];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[h][i] += p * vf[i];
+    }
+  }
+  // the wave's 64 / SEGS key groups summed with butterflies (same segment = lanes SEGS apart), then the 4 waves in LDS
+#pragma unroll
+  for (int o = SEGS; o < 64; o <<= 1)
+#pragma unroll
+    for (int h = 0; h < G; ++h)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[h][i] += __shfl_xor(acc[h][i], o, 64);
+  if (lane < SEGS) {
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+      s_acc[wv][h][2 * sg] = f32x4{acc[h][0], acc[h][1], acc[h][2], acc[h][3]};
+      s_acc[wv][h][2 * sg + 1] = f32x4{acc[h][4], acc[h][5], acc[h][6], acc[h][7]};
+    }
+  }
+  __syncthreads();
+  // ---- write the split's partials
+  for (int i = t; i < G * D / 4; i += kThreads) {
+    const int h = i / (D / 4), c = i % (D / 4);
+    f32x4 s = s_acc[0][h][c];
+#pragma unroll
+    for (int w = 1; w < kThreads / 64; ++w) s += s_acc[w][h][c];
+    reinterpret_cast<f32x4*>(po + ((int64_t)h * nsplit + split) * D)[c] = s;
+  }
+  if (t < G) {  // register arrays are not indexed by a runtime value (that would go through scratch)
+    float mt = 0.f, lt = 0.f;
+#pragma unroll
+    for (int h = 0; h < G; ++h) {
+      mt = (h == t) ? m[h] : mt;
+      lt = (h == t) ? l[h] : lt;
+    }
+    pml[(t * nsplit + split) * 2] = mt;
+    pml[(t * nsplit + split) * 2 + 1] = lt;
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(D / 2) decode_attn_combine_kernel(const float* __restrict__ part_o,
+                                                                    const float* __restrict__ part_ml, int Hq,
+                                                                    int nsplit, bf16_t* __restrict__ o, int64_t os) {
+  // blockIdx.x = b * Hq + h; partials of head h live at (b, kvh, g) = row b * Hq + h in [B, Hkv, G] order
+  const int bh = blockIdx.x, t = threadIdx.x;
+  const float* ml = part_ml + (int64_t)bh * nsplit * 2;
+  const float* po = part_o + (int64_t)bh * nsplit * D;
+  float M = kNegBig;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ml[2 * s]);
+  float L = 0.f, a0 = 0.f, a1 = 0.f;
+  for (int s = 0; s < nsplit; ++s) {
+    const float w = ml[2 * s + 1] > 0.f ? exp2f(ml[2 * s] - M) : 0.f;
+    L += ml[2 * s + 1] * w;
+    a0 += po[(int64_t)s * D + 2 * t] * w;
+    a1 += po[(int64_t)s * D + 2 * t + 1] * w;
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  const int b = bh / Hq, h = bh % Hq;
+  *reinterpret_cast<uint32_t*>(o + (int64_t)b * os + (int64_t)h * D + 2 * t) = pack2(a0 * inv, a1 * inv);
+}
+
+int decode_attn_splits(int max_len) { return (max_len + kCH - 1) / kCH; }
+
+template <int D, int G>
+static void launch_split(const bf16_t* q, int64_t qs, const bf16_t* kc, const bf16_t* vc, const int* lens, int B,
+                         int Smax, int Hkv, float sl2, float* po, float* pml, int nsplit, hipStream_t stream) {
+  decode_attn_split_kernel<D, G><<<dim3(nsplit, B * Hkv), kThreads, 0, stream>>>(q, qs, kc, vc, lens, Smax, Hkv, sl2,
+                                                                                po, pml, nsplit);
+}
+
+int decode_attn(const bf16_t* q, int64_t qs, const bf16_t* kc, const bf16_t* vc, const int* lens, bf16_t* o,
+                int64_t os, float* part_o, float* part_ml, int B, int Smax, int Hq, int Hkv, int D, int nsplit,
+                float scale, hipStream_t stream) {
+  if (Hq % Hkv != 0 || nsplit < 1 || nsplit * kCH > Smax + kCH - 1 || qs % 8 != 0 || os % 2 != 0) return -1;
+  const int G = Hq / Hkv;
+  const float sl2 = scale * kLog2e;
+#define DEC_CASE(DV, GV)                                                                                     \
+  if (D == DV && G == GV) {                                                                                  \
+    launch_split<DV, GV>(q, qs, kc, vc, lens, B, Smax, Hkv, sl2, part_o, part_ml, nsplit, stream);           \
+    decode_attn_combine_kernel<DV><<<B * Hq, DV / 2, 0, stream>>>(part_o, part_ml, Hq, nsplit, o, os);       \
+    return 0;                                                                                                \
+  }
+  DEC_CASE(128, 1)
+  DEC_CASE(128, 2)
+  DEC_CASE(128, 4)
+  DEC_CASE(128, 8)
+  DEC_CASE(64, 1)
+  DEC_CASE(64, 2)
+  DEC_CASE(64, 4)
+  DEC_CASE(64, 8)
+#undef DEC_CASE
+  return -2;
+}
+
+}  // namespace kop

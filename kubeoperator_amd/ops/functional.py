@@ -620,6 +620,26 @@ def flash_attention(q, k, v, B, S, Hq, Hkv, D, causal=True, scale=None):
     return o, lse.view(B, Hq, S)
 
 
+def decode_attention(q, k_cache, v_cache, lens, max_len: int, scale=None):
+    """Serving: attention of one new query row per sequence (q [B, Hq*D], a row view of the fused QKV output)
+    over its KV cache ([B, Smax, Hkv, D], ``lens`` [B] int32 valid keys, ``max_len`` >= every lens on the host).
+    HIP split-K kernel on the GPU (csrc/decode_attn.hip); forward only."""
+    D = k_cache.shape[-1]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if not q.is_cuda:
+        return ref.decode_attention_ref(q, k_cache, v_cache, lens, scale)
+    return _lib().decode_attn(q, k_cache, v_cache, lens, int(max_len), scale)
+
+
+def rope_positions_(x, cos, sin, pos, nheads, D):
+    """RoPE in place on the first ``nheads`` heads of each row of x at explicit positions ``pos`` [T] int32."""
+    if not x.is_cuda:
+        x.copy_(ref.rope_ref(x, cos, sin, 1, nheads, D, pos=pos))
+        return x
+    _lib().rope_(x, cos, sin, pos, 1, nheads, D, False)
+    return x
+
+
 # ---------------------------------------------------------------------------------------------------
 # embedding
 # ---------------------------------------------------------------------------------------------------

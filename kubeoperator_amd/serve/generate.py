@@ -1,0 +1,139 @@
+"""KV-cache generation for the Llama family on the gfx950 kernels (serving / evaluation of a trained chart).
+
+Prefill runs the prompt through the training forward's kernels (fused residual + RMSNorm, one QKV GEMM, RoPE
+in place, the flash-attention forward, SwiGLU MLP) and writes each layer's rotated K and V into a
+preallocated cache; every decode step then pushes one token per sequence through the same projections with
+RoPE at the sequence's position and the split-K decode-attention kernel (``csrc/decode_attn.hip``) over the
+cache. MI355X-first sizing: the cache is one contiguous [B, Smax, Hkv, D] bf16 tensor per layer for K and for
+V (Llama-3-8B: 128 KiB per token across its 32 layers, so 288 GB of HBM minus 16 GB of weights holds ~2M
+cached tokens, e.g. 256 sequences x 8k context), allocated once, never reshaped or copied between steps.
+
+Weights are the model's own parameters (views into a trainer's flat store, or any loaded Llama module); the
+generator adds no autograd state (``torch.no_grad``). On CPU every op falls back to its PyTorch reference.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..models.llama import Llama
+from ..ops import functional as kf
+from ..ops import reference as ref
+
+
+class KVCache:
+    def __init__(self, n_layers: int, batch: int, max_seq: int, n_kv_heads: int, head_dim: int, device,
+                 dtype=torch.bfloat16):
+        shape = (batch, max_seq, n_kv_heads, head_dim)
+        self.k = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(n_layers)]
+        self.v = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(n_layers)]
+        self.lens = torch.zeros(batch, dtype=torch.int32, device=device)
+        self.max_len = 0  # host copy of max(lens): sizes the decode kernel's split grid without a sync
+        self.batch, self.max_seq = batch, max_seq
+
+    def bytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in self.k + self.v)
+
+
+class LlamaGenerator:
+    def __init__(self, model: Llama, max_batch: int, max_seq: int):
+        if not isinstance(model, Llama) or model.tp.enabled:
+            raise ValueError("the generator serves single-GPU Llama models")
+        self.model = model
+        c = model.cfg
+        self.cfg = c
+        self.device = model.tok_emb.device
+        self.cache = KVCache(c.n_layers, max_batch, max_seq, c.n_kv_heads, c.head_dim, self.device)
+        self.cos, self.sin = ref.rope_cache(max_seq, c.head_dim, c.rope_theta, device=self.device)
+        self.scale = 1.0 / math.sqrt(c.head_dim)
+
+    def _head(self):
+        return self.model.tok_emb if self.cfg.tie_embeddings else self.model.lm_head
+
+    def _mlp(self, blk, y2):
+        return kf.swiglu_mlp(y2, blk.w_gate_up, blk.w_down)
+
+    @torch.no_grad()
+    def prefill(self, ids: torch.Tensor) -> torch.Tensor:
+        """Prompts ``ids`` [B, S] (one length for the batch) -> logits of the last position [B, vocab] (fp32)."""
+        c, m = self.cfg, self.model
+        B, S = ids.shape
+        if B > self.cache.batch or S > self.cache.max_seq:
+            raise ValueError("prompt batch / length exceeds the cache")
+        Hq, Hkv, D = c.n_heads, c.n_kv_heads, c.head_dim
+        a, kc = Hq * D, (Hq + Hkv) * D
+        x = kf.embedding(ids.reshape(-1), m.tok_emb)
+        pending = None
+        for i, blk in enumerate(m.layers):
+            if pending is None:
+                y, x1 = kf.rms_norm(x, blk.attn_norm, c.norm_eps), x
+            else:
+                y, x1 = kf.rms_norm(x, blk.attn_norm, c.norm_eps, residual=pending)
+            qkv = kf.linear(y, blk.wqkv)
+            if qkv.is_cuda:
+                from ..ops import load
+
+                load().rope_(qkv, self.cos, self.sin, None, S, Hq + Hkv, D, False)
+            else:
+                qkv = ref.rope_ref(qkv, self.cos, self.sin, S, Hq + Hkv, D)
+            q, k, v = qkv[:, :a], qkv[:, a:kc], qkv[:, kc:]
+            self.cache.k[i][:B, :S].copy_(k.reshape(B, S, Hkv, D))
+            self.cache.v[i][:B, :S].copy_(v.reshape(B, S, Hkv, D))
+            if q.is_cuda and S % 128 == 0:  # the HIP flash forward's tile constraint
+                o, _ = kf.flash_attention(q, k, v, B, S, Hq, Hkv, D, causal=True, scale=self.scale)
+            else:
+                o, _ = ref.attention_ref(q, k, v, B, S, Hq, Hkv, D, True, self.scale)
+            y2, x = kf.rms_norm(x1, blk.mlp_norm, c.norm_eps, residual=kf.linear(o, blk.wo))
+            pending = self._mlp(blk, y2)
+        y, _ = kf.rms_norm(x, m.final_norm, c.norm_eps, residual=pending)
+        self.cache.lens[:B] = S
+        self.cache.max_len = S
+        last = y.view(B, S, -1)[:, -1]
+        return torch.mm(last, self._head().t()).float()
+
+    @torch.no_grad()
+    def decode(self, tok: torch.Tensor) -> torch.Tensor:
+        """One new token per sequence ``tok`` [B] at position lens[b] -> next-token logits [B, vocab] (fp32)."""
+        c, m = self.cfg, self.model
+        B = tok.shape[0]
+        if self.cache.max_len + 1 > self.cache.max_seq:
+            raise ValueError("KV cache is full")
+        Hq, Hkv, D = c.n_heads, c.n_kv_heads, c.head_dim
+        a, kc = Hq * D, (Hq + Hkv) * D
+        pos = self.cache.lens[:B].clone()
+        rows = torch.arange(B, device=self.device)
+        pl = pos.long()
+        lens = pos + 1
+        max_len = self.cache.max_len + 1
+        x = kf.embedding(tok.reshape(-1), m.tok_emb)
+        pending = None
+        for i, blk in enumerate(m.layers):
+            if pending is None:
+                y, x1 = kf.rms_norm(x, blk.attn_norm, c.norm_eps), x
+            else:
+                y, x1 = kf.rms_norm(x, blk.attn_norm, c.norm_eps, residual=pending)
+            qkv = kf.linear(y, blk.wqkv)
+            kf.rope_positions_(qkv, self.cos, self.sin, pos, Hq + Hkv, D)
+            self.cache.k[i][rows, pl] = qkv[:, a:kc].reshape(B, Hkv, D)
+            self.cache.v[i][rows, pl] = qkv[:, kc:].reshape(B, Hkv, D)
+            o = kf.decode_attention(qkv[:, :a], self.cache.k[i][:B], self.cache.v[i][:B], lens, max_len, self.scale)
+            y2, x = kf.rms_norm(x1, blk.mlp_norm, c.norm_eps, residual=kf.linear(o, blk.wo))
+            pending = self._mlp(blk, y2)
+        y, _ = kf.rms_norm(x, m.final_norm, c.norm_eps, residual=pending)
+        self.cache.lens[:B] = lens
+        self.cache.max_len = max_len
+        return torch.mm(y, self._head().t()).float()
+
+    @torch.no_grad()
+    def generate(self, ids: torch.Tensor, max_new_tokens: int) -> torch.Tensor:
+        """Greedy continuation: [B, S] prompt -> [B, S + max_new_tokens] tokens."""
+        out = [ids]
+        logits = self.prefill(ids)
+        for _ in range(max_new_tokens):
+            nxt = logits.argmax(-1)
+            out.append(nxt.unsqueeze(1).to(ids.dtype))
+            if len(out) - 1 == max_new_tokens:
+                break
+            logits = self.decode(nxt)
+        return torch.cat(out, dim=1)

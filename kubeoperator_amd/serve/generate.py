@@ -37,7 +37,11 @@ class KVCache:
 
 
 class LlamaGenerator:
-    def __init__(self, model: Llama, max_batch: int, max_seq: int):
+    """``graph``: replay each decode step as one captured HIP graph (``torch.cuda.CUDAGraph`` is a hipGraph on
+    ROCm) -- a decode step is ~400 small launches whose host-side cost dominates at small batch. The graph's
+    decode-attention grid then covers the whole cache (splits past a sequence's length exit at once)."""
+
+    def __init__(self, model: Llama, max_batch: int, max_seq: int, graph: bool = False):
         if not isinstance(model, Llama) or model.tp.enabled:
             raise ValueError("the generator serves single-GPU Llama models")
         self.model = model
@@ -47,6 +51,8 @@ class LlamaGenerator:
         self.cache = KVCache(c.n_layers, max_batch, max_seq, c.n_kv_heads, c.head_dim, self.device)
         self.cos, self.sin = ref.rope_cache(max_seq, c.head_dim, c.rope_theta, device=self.device)
         self.scale = 1.0 / math.sqrt(c.head_dim)
+        self.graph = graph and self.device.type == "cuda"
+        self._graphs: dict = {}  # batch -> (graph, static token input, static logits output)
 
     def _head(self):
         return self.model.tok_emb if self.cfg.tie_embeddings else self.model.lm_head
@@ -95,17 +101,46 @@ class LlamaGenerator:
     @torch.no_grad()
     def decode(self, tok: torch.Tensor) -> torch.Tensor:
         """One new token per sequence ``tok`` [B] at position lens[b] -> next-token logits [B, vocab] (fp32)."""
-        c, m = self.cfg, self.model
         B = tok.shape[0]
         if self.cache.max_len + 1 > self.cache.max_seq:
             raise ValueError("KV cache is full")
+        if not self.graph:
+            out = self._decode(tok, self.cache.max_len + 1)
+        else:
+            if B not in self._graphs:
+                self._capture(B, tok)
+            g, static_tok, static_out = self._graphs[B]
+            static_tok.copy_(tok)
+            g.replay()
+            out = static_out.clone()
+        self.cache.max_len += 1
+        return out
+
+    def _capture(self, B: int, tok: torch.Tensor) -> None:
+        static_tok = tok.clone()
+        lens0 = self.cache.lens.clone()
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):  # warm-up outside capture (library handles, workspaces); state restored below
+            self._decode(static_tok, self.cache.max_seq)
+        torch.cuda.current_stream().wait_stream(s)
+        self.cache.lens.copy_(lens0)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            static_out = self._decode(static_tok, self.cache.max_seq)
+        self.cache.lens.copy_(lens0)  # capture does not run the kernels, but keep the state exact either way
+        self._graphs[B] = (g, static_tok, static_out)
+
+    def _decode(self, tok: torch.Tensor, max_len: int) -> torch.Tensor:
+        """Device-side body of a decode step (no host reads: capturable); ``max_len`` sizes the split grid."""
+        c, m = self.cfg, self.model
+        B = tok.shape[0]
         Hq, Hkv, D = c.n_heads, c.n_kv_heads, c.head_dim
         a, kc = Hq * D, (Hq + Hkv) * D
         pos = self.cache.lens[:B].clone()
-        rows = torch.arange(B, device=self.device)
+        rows = self._rows(B)
         pl = pos.long()
         lens = pos + 1
-        max_len = self.cache.max_len + 1
         x = kf.embedding(tok.reshape(-1), m.tok_emb)
         pending = None
         for i, blk in enumerate(m.layers):
@@ -122,8 +157,13 @@ class LlamaGenerator:
             pending = self._mlp(blk, y2)
         y, _ = kf.rms_norm(x, m.final_norm, c.norm_eps, residual=pending)
         self.cache.lens[:B] = lens
-        self.cache.max_len = max_len
         return torch.mm(y, self._head().t()).float()
+
+    def _rows(self, B: int) -> torch.Tensor:
+        key = ("rows", B)
+        if key not in self._graphs:
+            self._graphs[key] = torch.arange(B, device=self.device)
+        return self._graphs[key]
 
     @torch.no_grad()
     def generate(self, ids: torch.Tensor, max_new_tokens: int) -> torch.Tensor:

@@ -23,8 +23,8 @@ def _model(device, seed=0):
     return m.to(device=device, dtype=torch.bfloat16)
 
 
-def _check_decode_matches_prefill(model, ref_model, S, steps, B=2):
-    gen = LlamaGenerator(model, max_batch=B, max_seq=S + steps + 1)
+def _check_decode_matches_prefill(model, ref_model, S, steps, B=2, graph=False):
+    gen = LlamaGenerator(model, max_batch=B, max_seq=S + steps + 1, graph=graph)
     ids = torch.randint(0, model.cfg.vocab_size, (B, S), generator=torch.Generator().manual_seed(1))
     dev = model.tok_emb.device
     seq = ids.to(dev)
@@ -66,8 +66,10 @@ def test_decode_attention_kernel_matches_reference(D, Hq, Hkv):
 
 
 @pytest.mark.gpu
-def test_generate_gpu_decode_matches_cpu_reference():
-    """HIP prefill (flash forward at S = 128) + HIP decode steps against the CPU reference path."""
+@pytest.mark.parametrize("graph", [False, True])
+def test_generate_gpu_decode_matches_cpu_reference(graph):
+    """HIP prefill (flash forward at S = 128) + HIP decode steps (eager, or replayed HIP graphs) against the CPU
+    reference path."""
     gpu = _model("cuda")
     cpu = _model("cpu")
-    _check_decode_matches_prefill(gpu, cpu, S=128, steps=5)
+    _check_decode_matches_prefill(gpu, cpu, S=128, steps=5, graph=graph)

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--batch", default="1,16,64")
     ap.add_argument("--prompt", type=int, default=2048)
     ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--graph", default="0,1", help="decode steps eager (0) and/or as replayed HIP graphs (1)")
     a = ap.parse_args()
     from kubeoperator_amd.models import build_model, get_config
     from kubeoperator_amd.ops import load
@@ -36,8 +37,8 @@ def main():
         for n, p in m.named_parameters():
             p.fill_(1.0) if "norm" in n else p.normal_(0.0, 0.02, generator=g)
     wbytes = sum(p.numel() * p.element_size() for p in m.parameters())
-    for B in [int(x) for x in a.batch.split(",")]:
-        gen = LlamaGenerator(m, max_batch=B, max_seq=a.prompt + a.steps + 1)
+    for B, graph in [(int(x), int(gr)) for x in a.batch.split(",") for gr in a.graph.split(",")]:
+        gen = LlamaGenerator(m, max_batch=B, max_seq=a.prompt + a.steps + 3, graph=bool(graph))
         ids = torch.randint(0, cfg.vocab_size, (B, a.prompt), device="cuda")
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -55,7 +56,7 @@ def main():
         dt = (time.perf_counter() - t0) / a.steps
         ctx = a.prompt + 2 + a.steps / 2  # mean cached length over the timed steps
         kv_bytes = B * ctx * cfg.n_layers * 2 * cfg.n_kv_heads * cfg.head_dim * 2
-        print(json.dumps({"bench": "decode", "model": a.model, "batch": B, "prompt": a.prompt,
+        print(json.dumps({"bench": "decode", "model": a.model, "batch": B, "prompt": a.prompt, "hip_graph": bool(graph),
                           "prefill_tokens_per_s": round(B * a.prompt / t_pre, 1), "decode_ms_per_step": round(dt * 1e3, 3),
                           "decode_tokens_per_s": round(B / dt, 1),
                           "hbm_gb_per_step": round((wbytes + kv_bytes) / 1e9, 2),

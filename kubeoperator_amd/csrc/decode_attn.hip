@@ -46,7 +46,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_split_kernel(
   const int b = blockIdx.y / Hkv, kvh = blockIdx.y % Hkv;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int kg = t / SEGS, sg = t % SEGS;
-  const int len = lens[b];
+  const int len = min(lens[b], Smax);  // never read past the cache, whatever the caller's lengths
   const int k0 = split * kCH;
   const int64_t rs = (int64_t)Hkv * D;  // cache row stride (elements) between consecutive keys
   const bf16_t* kbase = kc + ((int64_t)b * Smax) * rs + (int64_t)kvh * D + sg * 8;

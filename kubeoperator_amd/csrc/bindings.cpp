@@ -338,7 +338,7 @@ void flash_attn_bwd(const Tensor& q, const Tensor& k, const Tensor& v, const Ten
 }  // namespace
 
 // ------------------------------------------------------------------ decode attention (serving)
-// q: [B, Hq*D] rows (strided view allowed); k_cache / v_cache: [B, Smax, Hkv, D] contiguous; lens: [B] int32
+// q: [B, Hq*D] rows (strided view allowed); k_cache / v_cache: [B, Hkv, Smax, D] contiguous; lens: [B] int32
 // (valid keys per sequence, 1 <= lens <= Smax); max_len bounds lens (host value: sizes the split grid)
 Tensor decode_attn(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& lens, int64_t max_len,
                    double scale) {
@@ -347,11 +347,11 @@ Tensor decode_attn(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache
   check_bf16(v_cache, "v_cache");
   check_rows(q, "q");
   TORCH_CHECK(k_cache.dim() == 4 && k_cache.is_contiguous() && v_cache.is_contiguous() &&
-                  k_cache.sizes() == v_cache.sizes(), "caches must be contiguous [B, Smax, Hkv, D] and equal");
+                  k_cache.sizes() == v_cache.sizes(), "caches must be contiguous [B, Hkv, Smax, D] and equal");
   check_aligned(k_cache, "k_cache");
   check_aligned(v_cache, "v_cache");
   TORCH_CHECK(lens.is_cuda() && lens.scalar_type() == at::kInt && lens.is_contiguous(), "lens must be int32 on the GPU");
-  const int B = (int)k_cache.size(0), Smax = (int)k_cache.size(1), Hkv = (int)k_cache.size(2), D = (int)k_cache.size(3);
+  const int B = (int)k_cache.size(0), Hkv = (int)k_cache.size(1), Smax = (int)k_cache.size(2), D = (int)k_cache.size(3);
   TORCH_CHECK(q.size(0) == B && lens.numel() == B, "batch mismatch");
   TORCH_CHECK(q.size(1) % D == 0, "q width must be a multiple of head_dim");
   const int Hq = (int)(q.size(1) / D);

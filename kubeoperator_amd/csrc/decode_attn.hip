@@ -2,7 +2,8 @@
 // ("flash decoding") so a batch of a few sequences still fills the 256 CUs.
 //
 //   q      [B, Hq * D]           bf16 rows (row stride qs: the Q columns of the fused QKV projection)
-//   cache  K, V [B, Smax, Hkv, D] bf16, keys [0, len[b]) valid
+//   cache  K, V [B, Hkv, Smax, D] bf16, keys [0, len[b]) valid: a (sequence, KV head) owns one contiguous
+//          [Smax, D] slab, so a workgroup's 256-key chunk is one contiguous 64 KiB stream per tensor
 //   o      [B, Hq * D]           bf16
 //
 // Memory-bound: every step streams the whole live cache (Llama-3-8B, 8k context: 4 MiB of K+V per sequence
@@ -48,9 +49,9 @@ __global__ void __launch_bounds__(kThreads) decode_attn_split_kernel(
   const int kg = t / SEGS, sg = t % SEGS;
   const int len = min(lens[b], Smax);  // never read past the cache, whatever the caller's lengths
   const int k0 = split * kCH;
-  const int64_t rs = (int64_t)Hkv * D;  // cache row stride (elements) between consecutive keys
-  const bf16_t* kbase = kc + ((int64_t)b * Smax) * rs + (int64_t)kvh * D + sg * 8;
-  const bf16_t* vbase = vc + ((int64_t)b * Smax) * rs + (int64_t)kvh * D + sg * 8;
+  constexpr int64_t rs = D;  // cache row stride (elements) between consecutive keys of one KV head
+  const bf16_t* kbase = kc + ((int64_t)b * Hkv + kvh) * Smax * D + sg * 8;
+  const bf16_t* vbase = vc + ((int64_t)b * Hkv + kvh) * Smax * D + sg * 8;
   float* po = part_o + (((int64_t)b * Hkv + kvh) * G * nsplit) * D;  // [G][nsplit][D] for this (b, kvh)
   float* pml = part_ml + (((int64_t)b * Hkv + kvh) * G * nsplit) * 2;
   if (k0 >= len) {  // split past the sequence: an empty partial

@@ -69,7 +69,7 @@ int flash_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16
                    int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, int64_t dos, int64_t dqs,
                    int64_t dks, int64_t dvs, float scale, bool causal, hipStream_t stream);
 
-// decode_attn.hip: one query token per sequence against a [B, Smax, Hkv, D] KV cache (lens[b] valid keys),
+// decode_attn.hip: one query token per sequence against a [B, Hkv, Smax, D] KV cache (lens[b] valid keys),
 // split-K over 256-key chunks; part_o: B * Hq * nsplit * D floats, part_ml: B * Hq * nsplit * 2 floats
 int decode_attn_splits(int max_len);
 int decode_attn(const bf16_t* q, int64_t qs, const bf16_t* kc, const bf16_t* vc, const int* lens, bf16_t* o,

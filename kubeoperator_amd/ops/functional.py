@@ -622,7 +622,7 @@ def flash_attention(q, k, v, B, S, Hq, Hkv, D, causal=True, scale=None):
 
 def decode_attention(q, k_cache, v_cache, lens, max_len: int, scale=None):
     """Serving: attention of one new query row per sequence (q [B, Hq*D], a row view of the fused QKV output)
-    over its KV cache ([B, Smax, Hkv, D], ``lens`` [B] int32 valid keys, ``max_len`` >= every lens on the host).
+    over its KV cache ([B, Hkv, Smax, D], ``lens`` [B] int32 valid keys, ``max_len`` >= every lens on the host).
     HIP split-K kernel on the GPU (csrc/decode_attn.hip); forward only."""
     D = k_cache.shape[-1]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)

@@ -90,15 +90,15 @@ def adamw_ref(master, m, v, g, lr, b1, b2, eps, wd, step, gscale=1.0):
 
 
 def decode_attention_ref(q, k_cache, v_cache, lens, scale):
-    """One query row per sequence against its cache: q [B, Hq*D], caches [B, Smax, Hkv, D], lens [B] valid keys."""
-    B, _, Hkv, D = k_cache.shape
+    """One query row per sequence against its cache: q [B, Hq*D], caches [B, Hkv, Smax, D], lens [B] valid keys."""
+    B, Hkv, _, D = k_cache.shape
     Hq = q.shape[1] // D
     out = torch.empty(B, Hq * D, dtype=q.dtype, device=q.device)
     for b in range(B):
         n = int(lens[b])
         qh = q[b].float().view(Hq, 1, D)
-        kh = k_cache[b, :n].float().permute(1, 0, 2).repeat_interleave(Hq // Hkv, dim=0)  # [Hq, n, D]
-        vh = v_cache[b, :n].float().permute(1, 0, 2).repeat_interleave(Hq // Hkv, dim=0)
+        kh = k_cache[b, :, :n].float().repeat_interleave(Hq // Hkv, dim=0)  # [Hq, n, D]
+        vh = v_cache[b, :, :n].float().repeat_interleave(Hq // Hkv, dim=0)
         p = torch.softmax((qh @ kh.transpose(1, 2)) * scale, dim=-1)
         out[b] = (p @ vh).reshape(Hq * D).to(q.dtype)
     return out

@@ -4,8 +4,8 @@ Prefill runs the prompt through the training forward's kernels (fused residual +
 in place, the flash-attention forward, SwiGLU MLP) and writes each layer's rotated K and V into a
 preallocated cache; every decode step then pushes one token per sequence through the same projections with
 RoPE at the sequence's position and the split-K decode-attention kernel (``csrc/decode_attn.hip``) over the
-cache. MI355X-first sizing: the cache is one contiguous [B, Smax, Hkv, D] bf16 tensor per layer for K and for
-V (Llama-3-8B: 128 KiB per token across its 32 layers, so 288 GB of HBM minus 16 GB of weights holds ~2M
+cache. MI355X-first sizing: the cache is one contiguous [B, Hkv, Smax, D] bf16 tensor per layer for K and for
+V (each (sequence, KV head) a contiguous slab the decode kernel streams) (Llama-3-8B: 128 KiB per token across its 32 layers, so 288 GB of HBM minus 16 GB of weights holds ~2M
 cached tokens, e.g. 256 sequences x 8k context), allocated once, never reshaped or copied between steps.
 
 Weights are the model's own parameters (views into a trainer's flat store, or any loaded Llama module); the
@@ -25,7 +25,7 @@ from ..ops import reference as ref
 class KVCache:
     def __init__(self, n_layers: int, batch: int, max_seq: int, n_kv_heads: int, head_dim: int, device,
                  dtype=torch.bfloat16):
-        shape = (batch, max_seq, n_kv_heads, head_dim)
+        shape = (batch, n_kv_heads, max_seq, head_dim)
         self.k = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(n_layers)]
         self.v = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(n_layers)]
         self.lens = torch.zeros(batch, dtype=torch.int32, device=device)
@@ -84,8 +84,8 @@ class LlamaGenerator:
             else:
                 qkv = ref.rope_ref(qkv, self.cos, self.sin, S, Hq + Hkv, D)
             q, k, v = qkv[:, :a], qkv[:, a:kc], qkv[:, kc:]
-            self.cache.k[i][:B, :S].copy_(k.reshape(B, S, Hkv, D))
-            self.cache.v[i][:B, :S].copy_(v.reshape(B, S, Hkv, D))
+            self.cache.k[i][:B, :, :S].copy_(k.reshape(B, S, Hkv, D).transpose(1, 2))
+            self.cache.v[i][:B, :, :S].copy_(v.reshape(B, S, Hkv, D).transpose(1, 2))
             if q.is_cuda and S % 128 == 0:  # the HIP flash forward's tile constraint
                 o, _ = kf.flash_attention(q, k, v, B, S, Hq, Hkv, D, causal=True, scale=self.scale)
             else:
@@ -150,8 +150,8 @@ class LlamaGenerator:
                 y, x1 = kf.rms_norm(x, blk.attn_norm, c.norm_eps, residual=pending)
             qkv = kf.linear(y, blk.wqkv)
             kf.rope_positions_(qkv, self.cos, self.sin, pos, Hq + Hkv, D)
-            self.cache.k[i][rows, pl] = qkv[:, a:kc].reshape(B, Hkv, D)
-            self.cache.v[i][rows, pl] = qkv[:, kc:].reshape(B, Hkv, D)
+            self.cache.k[i][rows, :, pl] = qkv[:, a:kc].reshape(B, Hkv, D)
+            self.cache.v[i][rows, :, pl] = qkv[:, kc:].reshape(B, Hkv, D)
             o = kf.decode_attention(qkv[:, :a], self.cache.k[i][:B], self.cache.v[i][:B], lens, max_len, self.scale)
             y2, x = kf.rms_norm(x1, blk.mlp_norm, c.norm_eps, residual=kf.linear(o, blk.wo))
             pending = self._mlp(blk, y2)

@@ -54,8 +54,8 @@ def test_decode_attention_kernel_matches_reference(D, Hq, Hkv):
     torch.manual_seed(0)
     B, Smax = 5, 1300
     lens = torch.tensor([1, 255, 256, 700, 1300], dtype=torch.int32, device="cuda")
-    kc = torch.randn(B, Smax, Hkv, D, device="cuda").to(torch.bfloat16)
-    vc = torch.randn(B, Smax, Hkv, D, device="cuda").to(torch.bfloat16)
+    kc = torch.randn(B, Hkv, Smax, D, device="cuda").to(torch.bfloat16)
+    vc = torch.randn(B, Hkv, Smax, D, device="cuda").to(torch.bfloat16)
     qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda").to(torch.bfloat16)
     q = qkv[:, : Hq * D]  # strided row view, as the generator passes it
     scale = 1.0 / math.sqrt(D)

@@ -22,12 +22,17 @@ def main():
     ap.add_argument("--prompt", type=int, default=2048)
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--graph", default="0,1", help="decode steps eager (0) and/or as replayed HIP graphs (1)")
+    ap.add_argument("--gemm-tuning", default="use", choices=["off", "use", "tune"],
+                    help="TunableOp winners for the decode GEMM shapes (small M = batch): read, or re-tune into --gemm-results")
+    ap.add_argument("--gemm-results", default="")
     a = ap.parse_args()
     from kubeoperator_amd.models import build_model, get_config
     from kubeoperator_amd.ops import load
     from kubeoperator_amd.serve import LlamaGenerator
+    from kubeoperator_amd.train import gemm_tuning
 
     load()
+    tuning = gemm_tuning.setup(a.gemm_tuning, path=a.gemm_results or gemm_tuning.results_path("gfx950_decode"))
     cfg = get_config(a.model)
     with torch.device("meta"):
         m = build_model(cfg)
@@ -61,7 +66,7 @@ def main():
                           "decode_tokens_per_s": round(B / dt, 1),
                           "hbm_gb_per_step": round((wbytes + kv_bytes) / 1e9, 2),
                           "effective_tb_per_s": round((wbytes + kv_bytes) / dt / 1e12, 2),
-                          "kv_cache_gb": round(gen.cache.bytes() / 1e9, 2)}), flush=True)
+                          "kv_cache_gb": round(gen.cache.bytes() / 1e9, 2), "gemm_selection": tuning}), flush=True)
         del gen
         torch.cuda.empty_cache()
 

@@ -11,7 +11,8 @@
 // G = Hq / Hkv query heads of its group, not around matrix cores (M = G <= 8 query rows per key tile would
 // leave MFMA 32-row tiles mostly empty).
 //
-// Pass 1: grid (splits, B * Hkv), 256 threads. A workgroup owns CH = 256 keys of one (sequence, KV head).
+// Pass 1: grid (splits, B * Hkv), 256 threads. A workgroup owns CH = 128 keys (KOP_DECODE_CH=256: 256) of one
+// (sequence, KV head).
 //   thread t = (key group kg = t / 16, segment sg = t % 16): the 16 threads of a key group read one 256-byte
 //   K row (D = 128) as 16 x 16 B -- a wave loads 4 whole rows per instruction -- and each keeps G partial dot
 //   products of its 8 dims, summed over the 16 lanes with 4 butterfly shuffles. Scores (already scaled by
@@ -21,26 +22,28 @@
 //   over the 4 waves in LDS. Output per split: unnormalised acc [G, D], running max m and sum l (fp32).
 // Pass 2: grid B * Hq, D / 2 threads: o = sum_s acc_s 2^(m_s - M) / sum_s l_s 2^(m_s - M).
 #include "common.h"
+#include <cstdlib>
 #include "kernels.h"
 
 namespace kop {
 
 namespace {
-constexpr int kCH = 256;          // keys per workgroup (one split)
 constexpr int kThreads = 256;
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kNegBig = -1e30f;
 }  // namespace
 
-template <int D, int G>
+// CH keys per workgroup (one split): 256 (16 K + 16 V row segments in flight per thread, ~180 VGPRs, two
+// workgroups per CU) or 128 (8 + 8, more workgroups per CU to overlap one's softmax with another's loads)
+template <int D, int G, int CH>
 __global__ void __launch_bounds__(kThreads) decode_attn_split_kernel(
     const bf16_t* __restrict__ q, int64_t qs, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
     const int* __restrict__ lens, int Smax, int Hkv, float scale_log2, float* __restrict__ part_o,
     float* __restrict__ part_ml, int nsplit) {
   constexpr int SEGS = D / 8;         // 16-byte segments per row (16 at D = 128, 8 at D = 64)
   constexpr int KG = kThreads / SEGS; // key groups (16 / 32)
-  constexpr int KPT = kCH / KG;       // keys per thread (16 / 8)
-  __shared__ float s_p[G][kCH];       // scores, then probabilities
+  constexpr int KPT = CH / KG;        // keys per thread (16 / 8 at CH 256)
+  __shared__ float s_p[G][CH];        // scores, then probabilities
   __shared__ float s_red[G][kThreads / 64];
   __shared__ f32x4 s_acc[kThreads / 64][G][D / 4];
   const int split = blockIdx.x;
@@ -48,7 +51,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_split_kernel(
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int kg = t / SEGS, sg = t % SEGS;
   const int len = min(lens[b], Smax);  // never read past the cache, whatever the caller's lengths
-  const int k0 = split * kCH;
+  const int k0 = split * CH;
   constexpr int64_t rs = D;  // cache row stride (elements) between consecutive keys of one KV head
   const bf16_t* kbase = kc + ((int64_t)b * Hkv + kvh) * Smax * D + sg * 8;
   const bf16_t* vbase = vc + ((int64_t)b * Hkv + kvh) * Smax * D + sg * 8;
@@ -108,11 +111,11 @@ __global__ void __launch_bounds__(kThreads) decode_attn_split_kernel(
     }
   }
   __syncthreads();
-  // ---- per-head max and sum over the CH keys (thread t covers key t of every head)
+  // ---- per-head max and sum over the CH keys (thread t covers key t of every head; CH <= 256 threads)
   float m[G], l[G];
 #pragma unroll
   for (int h = 0; h < G; ++h) {
-    const float mv = wave_max(s_p[h][t]);
+    const float mv = wave_max(t < CH ? s_p[h][t] : kNegBig);
     if (lane == 0) s_red[h][wv] = mv;
   }
   __syncthreads();
@@ -126,9 +129,9 @@ __global__ void __launch_bounds__(kThreads) decode_attn_split_kernel(
   __syncthreads();
 #pragma unroll
   for (int h = 0; h < G; ++h) {
-    const float s = s_p[h][t];
+    const float s = t < CH ? s_p[h][t] : kNegBig;
     const float p = s <= 0.5f * kNegBig ? 0.f : exp2f(s - m[h]);
-    s_p[h][t] = p;
+    if (t < CH) s_p[h][t] = p;
     const float sv = wave_sum(p);
     if (lane == 0) s_red[h][wv] = sv;
   }
@@ -215,19 +218,32 @@ __global__ void __launch_bounds__(D / 2) decode_attn_combine_kernel(const float*
   *reinterpret_cast<uint32_t*>(o + (int64_t)b * os + (int64_t)h * D + 2 * t) = pack2(a0 * inv, a1 * inv);
 }
 
-int decode_attn_splits(int max_len) { return (max_len + kCH - 1) / kCH; }
+static int chunk_keys() {
+  static const int ch = [] {
+    const char* e = getenv("KOP_DECODE_CH");  // 128 (default): -2 % per step at batch 128 vs 256, same at 64
+    return (e && atoi(e) == 256) ? 256 : 128;
+  }();
+  return ch;
+}
+
+int decode_attn_splits(int max_len) { return (max_len + chunk_keys() - 1) / chunk_keys(); }
 
 template <int D, int G>
 static void launch_split(const bf16_t* q, int64_t qs, const bf16_t* kc, const bf16_t* vc, const int* lens, int B,
                          int Smax, int Hkv, float sl2, float* po, float* pml, int nsplit, hipStream_t stream) {
-  decode_attn_split_kernel<D, G><<<dim3(nsplit, B * Hkv), kThreads, 0, stream>>>(q, qs, kc, vc, lens, Smax, Hkv, sl2,
-                                                                                po, pml, nsplit);
+  if (chunk_keys() == 128)
+    decode_attn_split_kernel<D, G, 128><<<dim3(nsplit, B * Hkv), kThreads, 0, stream>>>(q, qs, kc, vc, lens, Smax, Hkv,
+                                                                                       sl2, po, pml, nsplit);
+  else
+    decode_attn_split_kernel<D, G, 256><<<dim3(nsplit, B * Hkv), kThreads, 0, stream>>>(q, qs, kc, vc, lens, Smax, Hkv,
+                                                                                       sl2, po, pml, nsplit);
 }
 
 int decode_attn(const bf16_t* q, int64_t qs, const bf16_t* kc, const bf16_t* vc, const int* lens, bf16_t* o,
                 int64_t os, float* part_o, float* part_ml, int B, int Smax, int Hq, int Hkv, int D, int nsplit,
                 float scale, hipStream_t stream) {
-  if (Hq % Hkv != 0 || nsplit < 1 || nsplit * kCH > Smax + kCH - 1 || qs % 8 != 0 || os % 2 != 0) return -1;
+  const int ch = chunk_keys();
+  if (Hq % Hkv != 0 || nsplit < 1 || nsplit * ch > Smax + ch - 1 || qs % 8 != 0 || os % 2 != 0) return -1;
   const int G = Hq / Hkv;
   const float sl2 = scale * kLog2e;
 #define DEC_CASE(DV, GV)                                                                                     \

@@ -153,8 +153,11 @@ def _fwd8(x2, w):
     if w8 is not None:
         from . import fp8
 
+        M = x2.shape[0]
+        if M % 16:  # hipBLASLt's E4M3 GEMMs want 16-row multiples: pad (decode steps of a few sequences)
+            x2 = torch.cat([x2, x2.new_zeros(16 - M % 16, x2.shape[1])])
         x8, sx = fp8.quantize(x2)
-        return fp8.mm8(x8, sx, w8.t(), w.w8_scale, out_dtype=x2.dtype), sx
+        return fp8.mm8(x8, sx, w8.t(), w.w8_scale, out_dtype=x2.dtype)[:M], sx
     return torch.mm(x2, w.t()), None
 
 

@@ -41,10 +41,20 @@ class LlamaGenerator:
     ROCm) -- a decode step is ~400 small launches whose host-side cost dominates at small batch. The graph's
     decode-attention grid then covers the whole cache (splits past a sequence's length exit at once)."""
 
-    def __init__(self, model: Llama, max_batch: int, max_seq: int, graph: bool = False):
+    def __init__(self, model: Llama, max_batch: int, max_seq: int, graph: bool = False, fp8: bool = False):
+        """``fp8``: E4M3 copies of the four block projections (per-tensor scale) are attached to the model's
+        weights (``w.w8``, read by ``ops.functional`` linear / swiglu_mlp): decode steps then read half the weight
+        bytes. Serving-only models: a trainer would pick the copies up too (``drop_fp8`` removes them)."""
         if not isinstance(model, Llama) or model.tp.enabled:
             raise ValueError("the generator serves single-GPU Llama models")
         self.model = model
+        if fp8:
+            from ..ops import fp8 as f8
+
+            with torch.no_grad():
+                for blk in model.layers:
+                    for w in (blk.wqkv, blk.wo, blk.w_gate_up, blk.w_down):
+                        w.w8, w.w8_scale = f8.quantize(w.detach())
         c = model.cfg
         self.cfg = c
         self.device = model.tok_emb.device
@@ -53,6 +63,13 @@ class LlamaGenerator:
         self.scale = 1.0 / math.sqrt(c.head_dim)
         self.graph = graph and self.device.type == "cuda"
         self._graphs: dict = {}  # batch -> (graph, static token input, static logits output)
+
+    def drop_fp8(self) -> None:
+        for blk in self.model.layers:
+            for w in (blk.wqkv, blk.wo, blk.w_gate_up, blk.w_down):
+                for a in ("w8", "w8_scale"):
+                    if hasattr(w, a):
+                        delattr(w, a)
 
     def _head(self):
         return self.model.tok_emb if self.cfg.tie_embeddings else self.model.lm_head

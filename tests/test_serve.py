@@ -73,3 +73,22 @@ def test_generate_gpu_decode_matches_cpu_reference(graph):
     gpu = _model("cuda")
     cpu = _model("cpu")
     _check_decode_matches_prefill(gpu, cpu, S=128, steps=5, graph=graph)
+
+
+@pytest.mark.gpu
+def test_generate_gpu_fp8_weights_track_bf16():
+    """E4M3 block-projection weights (opt-in serving mode): decode logits stay close to the bf16 path."""
+    m = _model("cuda")
+    B, S = 3, 128  # 3 sequences: the E4M3 GEMMs pad to 16 rows
+    ids = torch.randint(0, m.cfg.vocab_size, (B, S), device="cuda", generator=torch.Generator(device="cuda").manual_seed(2))
+    outs = []
+    for fp8 in (False, True):
+        gen = LlamaGenerator(m, max_batch=B, max_seq=S + 4, fp8=fp8)
+        lg = gen.prefill(ids)
+        lg = gen.decode(lg.argmax(-1))
+        outs.append(lg.float())
+        gen.drop_fp8()
+    a, b = outs
+    cos = torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
+    assert cos > 0.99, cos
+    assert not hasattr(m.layers[0].wqkv, "w8")

@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--gemm-tuning", default="use", choices=["off", "use", "tune"],
                     help="TunableOp winners for the decode GEMM shapes (small M = batch): read, or re-tune into --gemm-results")
     ap.add_argument("--gemm-results", default="")
+    ap.add_argument("--fp8", default="0", help="0 and/or 1: E4M3 block-projection weights (opt-in serving mode)")
     a = ap.parse_args()
     from kubeoperator_amd.models import build_model, get_config
     from kubeoperator_amd.ops import load
@@ -42,8 +43,9 @@ def main():
         for n, p in m.named_parameters():
             p.fill_(1.0) if "norm" in n else p.normal_(0.0, 0.02, generator=g)
     wbytes = sum(p.numel() * p.element_size() for p in m.parameters())
-    for B, graph in [(int(x), int(gr)) for x in a.batch.split(",") for gr in a.graph.split(",")]:
-        gen = LlamaGenerator(m, max_batch=B, max_seq=a.prompt + a.steps + 3, graph=bool(graph))
+    runs = [(int(x), int(gr), int(f)) for f in a.fp8.split(",") for x in a.batch.split(",") for gr in a.graph.split(",")]
+    for B, graph, f8 in runs:
+        gen = LlamaGenerator(m, max_batch=B, max_seq=a.prompt + a.steps + 3, graph=bool(graph), fp8=bool(f8))
         ids = torch.randint(0, cfg.vocab_size, (B, a.prompt), device="cuda")
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -61,12 +63,13 @@ def main():
         dt = (time.perf_counter() - t0) / a.steps
         ctx = a.prompt + 2 + a.steps / 2  # mean cached length over the timed steps
         kv_bytes = B * ctx * cfg.n_layers * 2 * cfg.n_kv_heads * cfg.head_dim * 2
-        print(json.dumps({"bench": "decode", "model": a.model, "batch": B, "prompt": a.prompt, "hip_graph": bool(graph),
+        print(json.dumps({"bench": "decode", "model": a.model, "batch": B, "prompt": a.prompt, "hip_graph": bool(graph), "weights": "e4m3 projections" if f8 else "bf16",
                           "prefill_tokens_per_s": round(B * a.prompt / t_pre, 1), "decode_ms_per_step": round(dt * 1e3, 3),
                           "decode_tokens_per_s": round(B / dt, 1),
                           "hbm_gb_per_step": round((wbytes + kv_bytes) / 1e9, 2),
                           "effective_tb_per_s": round((wbytes + kv_bytes) / dt / 1e12, 2),
                           "kv_cache_gb": round(gen.cache.bytes() / 1e9, 2), "gemm_selection": tuning}), flush=True)
+        gen.drop_fp8()
         del gen
         torch.cuda.empty_cache()
 

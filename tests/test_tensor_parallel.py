@@ -130,3 +130,49 @@ def test_llama3_70b_tp8_shards_fit_one_mi355x():
     assert blk(shard) * 8 == blk(full) and rest(shard) == rest(full)
     per_rank = sum(p.numel() for p in shard.parameters())
     assert 16 * per_rank < 180e9, per_rank
+
+
+def _ckpt_worker(rank, world, tp, sp, init, ckpt, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      KOP_DIST_INIT=init)
+    torch.set_num_threads(1)
+    from kubeoperator_amd.parallel.dist import init_distributed, shutdown
+    from kubeoperator_amd.train import checkpoint
+
+    info = init_distributed("cpu")
+    a = Trainer(_tc(tp=tp, sp=sp, dp_mode="zero1"), info)
+    dpr, dp = a.dp_info.rank, a.dp_info.world
+    batches = [_batch(a.cfg.vocab_size, s, 2 * dp) for s in range(4)]
+    mine = [(ids[2 * dpr:2 * dpr + 2], tgt[2 * dpr:2 * dpr + 2]) for ids, tgt in batches]
+    for b in mine[:2]:
+        a.train_step([b])
+    checkpoint.save(a, ckpt, info)
+    for b in mine[2:]:
+        a.train_step([b])
+    # a second trainer resumes from the step-2 checkpoint and replays steps 3-4
+    b_ = Trainer(_tc(tp=tp, sp=sp, dp_mode="zero1", seed=99), info)
+    assert checkpoint.load(b_, ckpt, info) == 2
+    for b in mine[2:]:
+        b_.train_step([b])
+    same = bool(torch.equal(a.store.params, b_.store.params) and torch.equal(a.opt.exp_avg, b_.opt.exp_avg))
+    out_q.put((rank, same, sorted(os.listdir(ckpt))))
+    shutdown(info)
+
+
+@pytest.mark.parametrize("world,tp,sp", [(2, 2, False), (4, 2, True)])
+def test_tensor_parallel_checkpoint_resume_is_exact(world, tp, sp, tmp_path):
+    """Per-TP-rank checkpoint trees: a resumed TP (+SP, x DP with ZeRO-1) job continues bit-identically."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ckpt = str(tmp_path / "ckpt")
+    init = f"file://{tmp_path}/rdzv-ckpt"
+    procs = [ctx.Process(target=_ckpt_worker, args=(r, world, tp, sp, init, ckpt, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=600) for _ in range(world)]
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    for rank, same, listing in res:
+        assert same, rank
+        assert listing == [f"tp{t}_of{tp}" for t in range(tp)], listing

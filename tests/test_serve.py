@@ -92,3 +92,38 @@ def test_generate_gpu_fp8_weights_track_bf16():
     cos = torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
     assert cos > 0.99, cos
     assert not hasattr(m.layers[0].wqkv, "w8")
+
+
+def test_serving_http_endpoint_generates_greedy_tokens():
+    from fastapi.testclient import TestClient
+
+    from kubeoperator_amd.serve.server import create_app
+
+    m = _model("cpu")
+    c = TestClient(create_app(m, max_batch=2, max_seq=48))
+    assert c.get("/healthz").json() == {"ok": True}
+    assert c.get("/v1/model").json()["model"] == "tiny_llama"
+    prompt = [[1, 2, 3, 4, 5, 6], [7, 8, 9, 10, 11, 12]]
+    r = c.post("/v1/generate", json={"tokens": prompt, "max_new_tokens": 5})
+    assert r.status_code == 200, r.text
+    got = r.json()["tokens"]
+    want = LlamaGenerator(m, 2, 48).generate(torch.tensor(prompt), 5)[:, 6:].tolist()
+    assert got == want
+    assert c.post("/v1/generate", json={"tokens": [[1, 2], [3]], "max_new_tokens": 2}).status_code == 400
+    assert c.post("/v1/generate", json={"tokens": [[1] * 40], "max_new_tokens": 20}).status_code == 400
+    assert c.post("/v1/generate", json={"tokens": [[10 ** 6]], "max_new_tokens": 1}).status_code == 400
+
+
+def test_serving_loads_weights_from_a_training_checkpoint(tmp_path):
+    from kubeoperator_amd.parallel.dist import DistInfo
+    from kubeoperator_amd.serve.server import load_model
+    from kubeoperator_amd.train import TrainConfig, Trainer, checkpoint
+
+    tr = Trainer(TrainConfig(model="tiny_llama", micro_batch=2, seq_len=32, warmup_steps=1, total_steps=4), DistInfo())
+    ids = torch.randint(0, tr.cfg.vocab_size, (2, 33), generator=torch.Generator().manual_seed(0))
+    tr.train_step([(ids[:, :-1], ids[:, 1:])])
+    checkpoint.save(tr, str(tmp_path), DistInfo())
+    m = load_model("tiny_llama", "cpu", str(tmp_path))
+    want = dict(tr.store.named_params())
+    for n, p in m.named_parameters():
+        assert torch.equal(p, want[n].detach()), n

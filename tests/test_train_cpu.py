@@ -413,3 +413,17 @@ def test_training_chart_flags_exist_in_the_cli():
     src = open(cli.__file__).read()
     missing = [f for f in flags if f'"{f}"' not in src]
     assert not missing, missing
+
+
+def test_serving_chart_flags_exist_in_the_server_cli():
+    import re
+
+    from kubeoperator_amd.serve import server
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    dep = os.path.join(root, "kubeoperator_amd/control/resources/kubeasz/roles/kubeapps/files/charts/pytorch-rocm-serve/"
+                             "templates/deployment.yaml")
+    flags = set(re.findall(r"^\s*- (--[a-z0-9-]+)", open(dep).read(), re.M))
+    assert {"--model", "--max-batch", "--fp8", "--ckpt"} <= flags
+    src = open(server.__file__).read()
+    assert not [f for f in flags if f'"{f}"' not in src]

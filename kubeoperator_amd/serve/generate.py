@@ -29,8 +29,17 @@ class KVCache:
         self.k = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(n_layers)]
         self.v = [torch.zeros(shape, dtype=dtype, device=device) for _ in range(n_layers)]
         self.lens = torch.zeros(batch, dtype=torch.int32, device=device)
-        self.max_len = 0  # host copy of max(lens): sizes the decode kernel's split grid without a sync
+        self.host_lens = [0] * batch  # host mirror of lens: sizes the decode kernel's split grid without a sync
         self.batch, self.max_seq = batch, max_seq
+
+    @property
+    def max_len(self) -> int:
+        return max(self.host_lens)
+
+    def release(self, slot: int) -> None:
+        """Free a sequence slot (continuous batching): its next prefill overwrites the stale rows."""
+        self.host_lens[slot] = 0
+        self.lens[slot] = 0
 
     def bytes(self) -> int:
         return sum(t.numel() * t.element_size() for t in self.k + self.v)
@@ -78,12 +87,20 @@ class LlamaGenerator:
         return kf.swiglu_mlp(y2, blk.w_gate_up, blk.w_down)
 
     @torch.no_grad()
-    def prefill(self, ids: torch.Tensor) -> torch.Tensor:
-        """Prompts ``ids`` [B, S] (one length for the batch) -> logits of the last position [B, vocab] (fp32)."""
+    def prefill(self, ids: torch.Tensor, slot: int = 0) -> torch.Tensor:
+        """Prompts ``ids`` [B, S] (one length for the batch) into cache rows [slot, slot + B) -> logits of the
+        last position [B, vocab] (fp32)."""
         c, m = self.cfg, self.model
         B, S = ids.shape
-        if B > self.cache.batch or S > self.cache.max_seq:
+        if slot + B > self.cache.batch or S > self.cache.max_seq:
             raise ValueError("prompt batch / length exceeds the cache")
+        rows = slice(slot, slot + B)
+        S_real = S
+        if ids.is_cuda and S % 128 and S + 128 - S % 128 <= self.cache.max_seq:
+            # right-pad to the HIP flash forward's 128-row tiles: causal attention keeps the real positions
+            # independent of the padding, whose cache rows lie past lens and are overwritten by decode steps
+            ids = torch.cat([ids, ids.new_zeros(B, 128 - S % 128)], dim=1)
+            S = ids.shape[1]
         Hq, Hkv, D = c.n_heads, c.n_kv_heads, c.head_dim
         a, kc = Hq * D, (Hq + Hkv) * D
         x = kf.embedding(ids.reshape(-1), m.tok_emb)
@@ -101,8 +118,8 @@ class LlamaGenerator:
             else:
                 qkv = ref.rope_ref(qkv, self.cos, self.sin, S, Hq + Hkv, D)
             q, k, v = qkv[:, :a], qkv[:, a:kc], qkv[:, kc:]
-            self.cache.k[i][:B, :, :S].copy_(k.reshape(B, S, Hkv, D).transpose(1, 2))
-            self.cache.v[i][:B, :, :S].copy_(v.reshape(B, S, Hkv, D).transpose(1, 2))
+            self.cache.k[i][rows, :, :S].copy_(k.reshape(B, S, Hkv, D).transpose(1, 2))
+            self.cache.v[i][rows, :, :S].copy_(v.reshape(B, S, Hkv, D).transpose(1, 2))
             if q.is_cuda and S % 128 == 0:  # the HIP flash forward's tile constraint
                 o, _ = kf.flash_attention(q, k, v, B, S, Hq, Hkv, D, causal=True, scale=self.scale)
             else:
@@ -110,19 +127,27 @@ class LlamaGenerator:
             y2, x = kf.rms_norm(x1, blk.mlp_norm, c.norm_eps, residual=kf.linear(o, blk.wo))
             pending = self._mlp(blk, y2)
         y, _ = kf.rms_norm(x, m.final_norm, c.norm_eps, residual=pending)
-        self.cache.lens[:B] = S
-        self.cache.max_len = S
-        last = y.view(B, S, -1)[:, -1]
+        self.cache.lens[rows] = S_real
+        for r in range(slot, slot + B):
+            self.cache.host_lens[r] = S_real
+        last = y.view(B, S, -1)[:, S_real - 1]
         return torch.mm(last, self._head().t()).float()
 
     @torch.no_grad()
-    def decode(self, tok: torch.Tensor) -> torch.Tensor:
-        """One new token per sequence ``tok`` [B] at position lens[b] -> next-token logits [B, vocab] (fp32)."""
+    def decode(self, tok: torch.Tensor, active: list | None = None) -> torch.Tensor:
+        """One new token per sequence ``tok`` [B] (cache rows [0, B)) at position lens[b] -> next-token logits
+        [B, vocab] (fp32). ``active`` (host list of bools, continuous batching): only those rows advance; the
+        others compute throw-away rows of the same batched GEMMs."""
         B = tok.shape[0]
-        if self.cache.max_len + 1 > self.cache.max_seq:
+        rows = range(B) if active is None else [r for r in range(B) if active[r]]
+        if max((self.cache.host_lens[r] for r in rows), default=0) + 1 > self.cache.max_seq:
             raise ValueError("KV cache is full")
-        if not self.graph:
-            out = self._decode(tok, self.cache.max_len + 1)
+        max_len = max(self.cache.host_lens[:B]) + 1
+        if active is not None:
+            act = torch.tensor([bool(x) for x in active[:B]], dtype=torch.int32).to(self.device, non_blocking=True)
+            out = self._decode(tok, max_len, act)
+        elif not self.graph:
+            out = self._decode(tok, max_len)
         else:
             if B not in self._graphs:
                 self._capture(B, tok)
@@ -130,7 +155,8 @@ class LlamaGenerator:
             static_tok.copy_(tok)
             g.replay()
             out = static_out.clone()
-        self.cache.max_len += 1
+        for r in rows:
+            self.cache.host_lens[r] += 1
         return out
 
     def _capture(self, B: int, tok: torch.Tensor) -> None:
@@ -148,7 +174,7 @@ class LlamaGenerator:
         self.cache.lens.copy_(lens0)  # capture does not run the kernels, but keep the state exact either way
         self._graphs[B] = (g, static_tok, static_out)
 
-    def _decode(self, tok: torch.Tensor, max_len: int) -> torch.Tensor:
+    def _decode(self, tok: torch.Tensor, max_len: int, active: torch.Tensor | None = None) -> torch.Tensor:
         """Device-side body of a decode step (no host reads: capturable); ``max_len`` sizes the split grid."""
         c, m = self.cfg, self.model
         B = tok.shape[0]
@@ -173,7 +199,7 @@ class LlamaGenerator:
             y2, x = kf.rms_norm(x1, blk.mlp_norm, c.norm_eps, residual=kf.linear(o, blk.wo))
             pending = self._mlp(blk, y2)
         y, _ = kf.rms_norm(x, m.final_norm, c.norm_eps, residual=pending)
-        self.cache.lens[:B] = lens
+        self.cache.lens[:B] = lens if active is None else pos + active
         return torch.mm(y, self._head().t()).float()
 
     def _rows(self, B: int) -> torch.Tensor:

@@ -3,8 +3,10 @@
   python -m kubeoperator_amd.serve.server --model llama3_8b --max-batch 64 --max-seq 8192 --port 8000 [--ckpt DIR]
 
 ``POST /v1/generate`` ``{"tokens": [[id, ...], ...], "max_new_tokens": N}`` -> ``{"tokens": [[...]], "ms": ...}``:
-the prompts of one request (equal lengths) are prefilled together and decoded greedily as one batch; requests
-are served one at a time on the GPU (a lock around the generator). ``GET /v1/model`` describes the loaded model,
+greedy continuation of every prompt. Continuous batching (``ContinuousBatcher``): every prompt of every
+concurrent request takes a free sequence slot of the KV cache as soon as one is free (its own prefill), and one
+decode step advances all active slots together -- prompts of any length, joining and leaving between steps, so
+the decode GEMMs and the decode-attention kernel see the whole live batch (ragged cache lengths). ``GET /v1/model`` describes the loaded model,
 ``GET /healthz`` answers readiness probes. Token ids in, token ids out: the chart ships no tokenizer files.
 Weights are random-init unless ``--ckpt`` names a training checkpoint directory (the trainer's flat layout;
 loaded with ``torch.load(weights_only=True)``).
@@ -12,6 +14,7 @@ loaded with ``torch.load(weights_only=True)``).
 from __future__ import annotations
 
 import argparse
+import queue
 import threading
 import time
 
@@ -27,12 +30,107 @@ class GenerateRequest(BaseModel):
     max_new_tokens: int = 16
 
 
+class _Seq:
+    def __init__(self, prompt: list[int], max_new: int):
+        self.prompt, self.max_new = prompt, max_new
+        self.out: list[int] = []
+        self.done = threading.Event()
+        self.error: Exception | None = None
+
+
+class ContinuousBatcher:
+    """One scheduler thread owns the generator: admits queued sequences into free cache slots (prefill), then
+    runs one decode step over every active slot; a sequence leaves its slot once it has its tokens."""
+
+    def __init__(self, gen: LlamaGenerator):
+        self.gen = gen
+        self.q: queue.Queue = queue.Queue()
+        self.slots: list[_Seq | None] = [None] * gen.cache.batch
+        self.next_tok = [0] * gen.cache.batch
+        self.steps = 0
+        self._stop = False
+        self._thread = threading.Thread(target=self._loop, name="kop-serve-batcher", daemon=True)
+        self._thread.start()
+
+    def generate(self, prompts: list[list[int]], max_new: int) -> list[list[int]]:
+        seqs = [_Seq(p, max_new) for p in prompts]
+        for sq in seqs:
+            self.q.put(sq)
+        for sq in seqs:
+            sq.done.wait()
+            if sq.error is not None:
+                raise sq.error
+        return [sq.out for sq in seqs]
+
+    def close(self) -> None:
+        self._stop = True
+        self.q.put(None)
+        self._thread.join(10)
+
+    def _finish(self, slot: int) -> None:
+        sq = self.slots[slot]
+        self.slots[slot] = None
+        self.gen.cache.release(slot)
+        sq.done.set()
+
+    def _admit(self, sq: _Seq) -> None:
+        slot = self.slots.index(None)
+        self.slots[slot] = sq
+        try:
+            ids = torch.tensor([sq.prompt], dtype=torch.long, device=self.gen.device)
+            nxt = int(self.gen.prefill(ids, slot=slot).argmax(-1)[0])
+        except Exception as e:  # a bad request fails alone
+            sq.error = e
+            self._finish(slot)
+            return
+        sq.out.append(nxt)
+        self.next_tok[slot] = nxt
+        if len(sq.out) >= sq.max_new:
+            self._finish(slot)
+
+    def _loop(self) -> None:
+        while not self._stop:
+            # admit queued sequences while a slot is free; block on the queue only when nothing is running
+            while None in self.slots:
+                running = any(s is not None for s in self.slots)
+                try:
+                    item = self.q.get_nowait() if running else self.q.get(timeout=0.5)
+                except queue.Empty:
+                    break
+                if item is None:  # close()
+                    break
+                self._admit(item)
+            active = [s is not None for s in self.slots]
+            if not any(active):
+                continue
+            n = max(i for i, a in enumerate(active) if a) + 1  # rows [0, n) cover every active slot
+            try:
+                tok = torch.tensor(self.next_tok[:n], dtype=torch.long, device=self.gen.device)
+                nxt = self.gen.decode(tok, active=active[:n]).argmax(-1).tolist()
+            except Exception as e:  # fail the running sequences, keep serving
+                for i in range(n):
+                    if self.slots[i] is not None:
+                        self.slots[i].error = e
+                        self._finish(i)
+                continue
+            self.steps += 1
+            for i in range(n):
+                sq = self.slots[i]
+                if sq is None:
+                    continue
+                sq.out.append(nxt[i])
+                self.next_tok[i] = nxt[i]
+                if len(sq.out) >= sq.max_new:
+                    self._finish(i)
+
+
 def create_app(model, max_batch: int, max_seq: int, graph: bool = False, fp8: bool = False):
     from fastapi import FastAPI, HTTPException
 
     gen = LlamaGenerator(model, max_batch=max_batch, max_seq=max_seq, graph=graph, fp8=fp8)
-    lock = threading.Lock()
+    batcher = ContinuousBatcher(gen)
     app = FastAPI(title="KubeOperator-AMD serving", docs_url="/docs")
+    app.state.batcher = batcher
 
     @app.get("/healthz")
     def healthz():
@@ -42,25 +140,22 @@ def create_app(model, max_batch: int, max_seq: int, graph: bool = False, fp8: bo
     def info():
         c = model.cfg
         return {"model": c.name, "params": c.num_params(), "max_batch": max_batch, "max_seq": max_seq,
+                "active": sum(x is not None for x in batcher.slots), "decode_steps": batcher.steps,
                 "kv_cache_gb": round(gen.cache.bytes() / 1e9, 3), "hip_graph": gen.graph, "fp8_weights": fp8}
 
     @app.post("/v1/generate")
     def generate(req: GenerateRequest):
-        if not req.tokens or len({len(t) for t in req.tokens}) != 1:
-            raise HTTPException(400, "tokens: a non-empty batch of equal-length prompts")
-        B, S = len(req.tokens), len(req.tokens[0])
-        if B > max_batch or S < 1 or S + req.max_new_tokens > max_seq or req.max_new_tokens < 1:
-            raise HTTPException(400, f"batch <= {max_batch}, 1 <= prompt and prompt + max_new_tokens <= {max_seq}")
+        if not req.tokens:
+            raise HTTPException(400, "tokens: a non-empty list of prompts")
+        S = max(len(t) for t in req.tokens)
+        if min(len(t) for t in req.tokens) < 1 or S + req.max_new_tokens > max_seq or req.max_new_tokens < 1:
+            raise HTTPException(400, f"1 <= prompt length and prompt + max_new_tokens <= {max_seq}")
         vocab = model.cfg.vocab_size
         if any(t < 0 or t >= vocab for row in req.tokens for t in row):
             raise HTTPException(400, f"token ids must be in [0, {vocab})")
-        ids = torch.tensor(req.tokens, dtype=torch.long, device=gen.device)
-        with lock:
-            t0 = time.perf_counter()
-            out = gen.generate(ids, req.max_new_tokens)
-            new = out[:, S:].tolist()
-            ms = (time.perf_counter() - t0) * 1e3
-        return {"tokens": new, "ms": round(ms, 3)}
+        t0 = time.perf_counter()
+        new = batcher.generate(req.tokens, req.max_new_tokens)
+        return {"tokens": new, "ms": round((time.perf_counter() - t0) * 1e3, 3)}
 
     return app
 

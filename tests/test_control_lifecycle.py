@@ -182,6 +182,17 @@ def test_app_deploy_nginx_and_training_chart(control):
     apps = {a["release"]: a for a in clusters.list_apps("demo")}
     assert set(apps) == {"nginx", "llama-8x"} and apps["llama-8x"]["training"]["tokens_per_s"] > 0
 
+    # the serving chart (Deployment + Service around kubeoperator_amd.serve.server)
+    e = deploy.create("demo", "app-deploy", {"chart": "pytorch-rocm-serve", "release": "llama-serve",
+                                             "namespace": "serve", "values": {"maxBatch": 32, "fp8": True}},
+                      run="inline")
+    assert e["state"] == "SUCCESS", e["result_summary"]
+    assert any(c.startswith("helm upgrade --install llama-serve /opt/kubeoperator/charts/pytorch-rocm-serve")
+               for c in control.farm.commands("m1"))
+    assert b"maxBatch: 32" in control.farm.fs["m1"]["/opt/kubeoperator/charts/values/llama-serve.yaml"]
+    assert deploy.create("demo", "app-remove", {"release": "llama-serve", "namespace": "serve"},
+                         run="inline")["state"] == "SUCCESS"
+
     assert deploy.create("demo", "app-remove", {"release": "nginx"}, run="inline")["state"] == "SUCCESS"
     assert [a["release"] for a in clusters.list_apps("demo")] == ["llama-8x"]
     assert clusters.get_cluster("demo").status == "RUNNING"

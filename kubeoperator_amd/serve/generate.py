@@ -87,15 +87,19 @@ class LlamaGenerator:
         return kf.swiglu_mlp(y2, blk.w_gate_up, blk.w_down)
 
     @torch.no_grad()
-    def prefill(self, ids: torch.Tensor, slot: int = 0) -> torch.Tensor:
-        """Prompts ``ids`` [B, S] (one length for the batch) into cache rows [slot, slot + B) -> logits of the
-        last position [B, vocab] (fp32)."""
+    def prefill(self, ids: torch.Tensor, slot: int = 0, lengths: list | None = None,
+                slots: list | None = None) -> torch.Tensor:
+        """Prompts ``ids`` [B, S] into cache rows [slot, slot + B) (or the listed ``slots``) -> logits of each
+        prompt's last position [B, vocab] (fp32). ``lengths``: real lengths of right-padded rows (default S):
+        causal attention keeps every real position independent of the padding after it."""
         c, m = self.cfg, self.model
         B, S = ids.shape
-        if slot + B > self.cache.batch or S > self.cache.max_seq:
+        slots = list(range(slot, slot + B)) if slots is None else list(slots)
+        lengths = [S] * B if lengths is None else list(lengths)
+        if len(slots) != B or len(lengths) != B or max(slots) >= self.cache.batch or S > self.cache.max_seq:
             raise ValueError("prompt batch / length exceeds the cache")
-        rows = slice(slot, slot + B)
-        S_real = S
+        contiguous = slots == list(range(slots[0], slots[0] + B))
+        rows = slice(slots[0], slots[0] + B) if contiguous else torch.tensor(slots, device=self.device)
         if ids.is_cuda and S % 128 and S + 128 - S % 128 <= self.cache.max_seq:
             # right-pad to the HIP flash forward's 128-row tiles: causal attention keeps the real positions
             # independent of the padding, whose cache rows lie past lens and are overwritten by decode steps
@@ -127,10 +131,11 @@ class LlamaGenerator:
             y2, x = kf.rms_norm(x1, blk.mlp_norm, c.norm_eps, residual=kf.linear(o, blk.wo))
             pending = self._mlp(blk, y2)
         y, _ = kf.rms_norm(x, m.final_norm, c.norm_eps, residual=pending)
-        self.cache.lens[rows] = S_real
-        for r in range(slot, slot + B):
-            self.cache.host_lens[r] = S_real
-        last = y.view(B, S, -1)[:, S_real - 1]
+        lt = torch.tensor(lengths, dtype=torch.int32)
+        self.cache.lens[rows] = lt.to(self.device)
+        for r, n in zip(slots, lengths):
+            self.cache.host_lens[r] = int(n)
+        last = y.view(B, S, -1)[torch.arange(B, device=y.device), (lt.long() - 1).to(y.device)]
         return torch.mm(last, self._head().t()).float()
 
     @torch.no_grad()

@@ -73,33 +73,51 @@ class ContinuousBatcher:
         self.gen.cache.release(slot)
         sq.done.set()
 
-    def _admit(self, sq: _Seq) -> None:
-        slot = self.slots.index(None)
-        self.slots[slot] = sq
-        try:
-            ids = torch.tensor([sq.prompt], dtype=torch.long, device=self.gen.device)
-            nxt = int(self.gen.prefill(ids, slot=slot).argmax(-1)[0])
-        except Exception as e:  # a bad request fails alone
-            sq.error = e
-            self._finish(slot)
-            return
-        sq.out.append(nxt)
-        self.next_tok[slot] = nxt
-        if len(sq.out) >= sq.max_new:
-            self._finish(slot)
+    def _admit(self, seqs: list) -> None:
+        """Prefill newly admitted sequences into free slots, one batched prefill per padded length (prompts
+        right-padded to 128-token multiples, so sequences of similar lengths share the prefill GEMMs)."""
+        groups: dict[int, list] = {}
+        for sq in seqs:
+            slot = self.slots.index(None)
+            self.slots[slot] = sq
+            n = len(sq.prompt)
+            padded = -(-n // 128) * 128
+            groups.setdefault(padded if padded <= self.gen.cache.max_seq else n, []).append((slot, sq))
+        for S, members in groups.items():
+            try:
+                ids = torch.zeros(len(members), S, dtype=torch.long)
+                for r, (_, sq) in enumerate(members):
+                    ids[r, :len(sq.prompt)] = torch.tensor(sq.prompt, dtype=torch.long)
+                logits = self.gen.prefill(ids.to(self.gen.device), slots=[sl for sl, _ in members],
+                                          lengths=[len(sq.prompt) for _, sq in members])
+                nxt = logits.argmax(-1).tolist()
+            except Exception as e:  # a bad request fails alone
+                for slot, sq in members:
+                    sq.error = e
+                    self._finish(slot)
+                continue
+            for (slot, sq), t in zip(members, nxt):
+                sq.out.append(t)
+                self.next_tok[slot] = t
+                if len(sq.out) >= sq.max_new:
+                    self._finish(slot)
 
     def _loop(self) -> None:
         while not self._stop:
-            # admit queued sequences while a slot is free; block on the queue only when nothing is running
-            while None in self.slots:
-                running = any(s is not None for s in self.slots)
+            # admit queued sequences into the free slots; block on the queue only when nothing is running
+            new = []
+            free = self.slots.count(None)
+            while len(new) < free:
+                running = any(s is not None for s in self.slots) or new
                 try:
                     item = self.q.get_nowait() if running else self.q.get(timeout=0.5)
                 except queue.Empty:
                     break
                 if item is None:  # close()
                     break
-                self._admit(item)
+                new.append(item)
+            if new:
+                self._admit(new)
             active = [s is not None for s in self.slots]
             if not any(active):
                 continue

@@ -146,9 +146,11 @@ def test_serving_loads_weights_from_a_training_checkpoint(tmp_path):
         assert torch.equal(p, want[n].detach()), n
 
 
-def test_continuous_batching_matches_independent_generation():
+@pytest.mark.parametrize("max_seq", [40, 200])
+def test_continuous_batching_matches_independent_generation(max_seq):
     """More concurrent prompts (of different lengths and token budgets) than cache slots: each joins a free slot,
-    decodes beside the others with ragged cache lengths, and gets exactly its own greedy continuation."""
+    decodes beside the others with ragged cache lengths, and gets exactly its own greedy continuation. With
+    max_seq 200 the admitted prompts are right-padded to 128 tokens and prefilled together (per-row lengths)."""
     import threading
 
     from kubeoperator_amd.serve.server import ContinuousBatcher
@@ -158,7 +160,7 @@ def test_continuous_batching_matches_independent_generation():
     jobs = [(torch.randint(0, m.cfg.vocab_size, (n,), generator=g).tolist(), k)
             for n, k in ((7, 5), (12, 3), (3, 8), (9, 1), (5, 6))]
     want = [LlamaGenerator(m, 1, 40).generate(torch.tensor([p]), k)[0, len(p):].tolist() for p, k in jobs]
-    b = ContinuousBatcher(LlamaGenerator(m, max_batch=2, max_seq=40))
+    b = ContinuousBatcher(LlamaGenerator(m, max_batch=3, max_seq=max_seq))
     got = [None] * len(jobs)
 
     def run(i):

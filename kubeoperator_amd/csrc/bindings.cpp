@@ -367,6 +367,27 @@ Tensor decode_attn(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache
   return o;
 }
 
+// qkv: [B, (Hq + 2 Hkv) D] fused rows; caches [B, Hkv, Smax, D]; pos: [B] int32 (cache row to append at)
+void decode_rope_append_(const Tensor& qkv, const Tensor& cos_t, const Tensor& sin_t, const Tensor& pos,
+                         const Tensor& k_cache, const Tensor& v_cache, int64_t Hq) {
+  check_bf16(qkv, "qkv");
+  check_rows(qkv, "qkv");
+  check_f32(cos_t, "cos");
+  check_f32(sin_t, "sin");
+  check_bf16(k_cache, "k_cache");
+  check_bf16(v_cache, "v_cache");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.is_contiguous() && v_cache.is_contiguous() &&
+                  k_cache.sizes() == v_cache.sizes(), "caches must be contiguous [B, Hkv, Smax, D] and equal");
+  TORCH_CHECK(pos.is_cuda() && pos.scalar_type() == at::kInt && pos.is_contiguous(), "pos must be int32 on the GPU");
+  const int B = (int)qkv.size(0), Hkv = (int)k_cache.size(1), Smax = (int)k_cache.size(2), D = (int)k_cache.size(3);
+  TORCH_CHECK(k_cache.size(0) >= B && pos.numel() == B, "batch mismatch");
+  TORCH_CHECK(qkv.size(1) == (Hq + 2 * Hkv) * D, "qkv width must be (Hq + 2 Hkv) * D");
+  TORCH_CHECK(cos_t.size(0) >= Smax && cos_t.size(1) == D / 2, "rope tables must cover the cache");
+  rc(kop::decode_rope_append(bp(qkv), qkv.stride(0), cos_t.data_ptr<float>(), sin_t.data_ptr<float>(),
+                             pos.data_ptr<int>(), bp(k_cache), bp(v_cache), B, Smax, (int)Hq, Hkv, D, cur_stream()),
+     "decode_rope_append");
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "kubeoperator_amd gfx950 (MI355X) HIP kernels";
   m.attr("ARCH") = "gfx950";
@@ -391,6 +412,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("clip_coef_", &clip_coef_);
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("decode_attn", &decode_attn);
+  m.def("decode_rope_append_", &decode_rope_append_);
   m.def("flash_attn_bwd_workspace", &flash_attn_bwd_workspace);
   m.def("flash_attn_bwd", &flash_attn_bwd);
   m.def("flash_attn_set_dq_variant", [](int64_t v) { return (int64_t)kop::flash_attn_set_dq_variant((int)v); });

@@ -226,6 +226,70 @@ static int chunk_keys() {
   return ch;
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Decode-step append: RoPE at each sequence's position on its new Q and K heads (in place in the fused QKV row)
+// and the rotated K row + the V row written into the cache at that position -- one launch per layer instead of
+// a RoPE kernel and two scatter copies. grid (B, ceil(items / 256)); items per token: (Hq + Hkv) heads x D/16
+// rotary chunks (8 pairs each), then Hkv x D/8 16-byte V chunks.
+// ---------------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) decode_rope_append_kernel(bf16_t* __restrict__ qkv, int64_t qs,
+                                                                 const float* __restrict__ cos_t,
+                                                                 const float* __restrict__ sin_t,
+                                                                 const int* __restrict__ pos, bf16_t* __restrict__ kc,
+                                                                 bf16_t* __restrict__ vc, int Smax, int Hq, int Hkv,
+                                                                 int D) {
+  const int b = blockIdx.x;
+  const int item = blockIdx.y * blockDim.x + threadIdx.x;
+  const int half = D >> 1, per_head = half >> 3;
+  const int n_rot = (Hq + Hkv) * per_head, n_v = Hkv * (D >> 3);
+  if (item >= n_rot + n_v) return;
+  const int p = min(max(pos[b], 0), Smax - 1);
+  bf16_t* row = qkv + (int64_t)b * qs;
+  if (item < n_rot) {
+    const int h = item / per_head, j = item - h * per_head;
+    bf16_t* base = row + (int64_t)h * D + j * 8;
+    const f32x4* cp = reinterpret_cast<const f32x4*>(cos_t + (int64_t)p * half + j * 8);
+    const f32x4* sp = reinterpret_cast<const f32x4*>(sin_t + (int64_t)p * half + j * 8);
+    float a[8], c[8], o1[8], o2[8], bb[8], sn[8];
+    unpack8(*reinterpret_cast<const u32x4*>(base), a);
+    unpack8(*reinterpret_cast<const u32x4*>(base + half), bb);
+    const f32x4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      c[i] = c0[i];
+      c[i + 4] = c1[i];
+      sn[i] = s0[i];
+      sn[i + 4] = s1[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      o1[i] = a[i] * c[i] - bb[i] * sn[i];
+      o2[i] = bb[i] * c[i] + a[i] * sn[i];
+    }
+    const u32x4 lo = pack8(o1), hi = pack8(o2);
+    *reinterpret_cast<u32x4*>(base) = lo;
+    *reinterpret_cast<u32x4*>(base + half) = hi;
+    if (h >= Hq) {  // a K head: its rotated row goes to the cache
+      bf16_t* dst = kc + (((int64_t)b * Hkv + (h - Hq)) * Smax + p) * D + j * 8;
+      *reinterpret_cast<u32x4*>(dst) = lo;
+      *reinterpret_cast<u32x4*>(dst + half) = hi;
+    }
+  } else {
+    const int v = item - n_rot, vh = v / (D >> 3), ch = v - vh * (D >> 3);
+    const u32x4 val = *reinterpret_cast<const u32x4*>(row + (int64_t)(Hq + Hkv + vh) * D + ch * 8);
+    *reinterpret_cast<u32x4*>(vc + (((int64_t)b * Hkv + vh) * Smax + p) * D + ch * 8) = val;
+  }
+}
+
+int decode_rope_append(bf16_t* qkv, int64_t qs, const float* cos_t, const float* sin_t, const int* pos, bf16_t* kc,
+                       bf16_t* vc, int B, int Smax, int Hq, int Hkv, int D, hipStream_t stream) {
+  if (D % 16 != 0 || qs % 8 != 0) return -1;
+  const int items = (Hq + Hkv) * (D / 16) + Hkv * (D / 8);
+  decode_rope_append_kernel<<<dim3(B, (items + 255) / 256), 256, 0, stream>>>(qkv, qs, cos_t, sin_t, pos, kc, vc, Smax,
+                                                                              Hq, Hkv, D);
+  return 0;
+}
+
 int decode_attn_splits(int max_len) { return (max_len + chunk_keys() - 1) / chunk_keys(); }
 
 template <int D, int G>

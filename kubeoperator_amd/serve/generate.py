@@ -197,9 +197,14 @@ class LlamaGenerator:
             else:
                 y, x1 = kf.rms_norm(x, blk.attn_norm, c.norm_eps, residual=pending)
             qkv = kf.linear(y, blk.wqkv)
-            kf.rope_positions_(qkv, self.cos, self.sin, pos, Hq + Hkv, D)
-            self.cache.k[i][rows, :, pl] = qkv[:, a:kc].reshape(B, Hkv, D)
-            self.cache.v[i][rows, :, pl] = qkv[:, kc:].reshape(B, Hkv, D)
+            if qkv.is_cuda:  # one kernel: RoPE at pos on Q / K + K / V rows appended to the cache
+                from ..ops import load
+
+                load().decode_rope_append_(qkv, self.cos, self.sin, pos, self.cache.k[i], self.cache.v[i], Hq)
+            else:
+                kf.rope_positions_(qkv, self.cos, self.sin, pos, Hq + Hkv, D)
+                self.cache.k[i][rows, :, pl] = qkv[:, a:kc].reshape(B, Hkv, D)
+                self.cache.v[i][rows, :, pl] = qkv[:, kc:].reshape(B, Hkv, D)
             o = kf.decode_attention(qkv[:, :a], self.cache.k[i][:B], self.cache.v[i][:B], lens, max_len, self.scale)
             y2, x = kf.rms_norm(x1, blk.mlp_norm, c.norm_eps, residual=kf.linear(o, blk.wo))
             pending = self._mlp(blk, y2)

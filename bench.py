@@ -51,9 +51,10 @@ def main() -> int:
     ap.add_argument("--recompute", type=int, default=0, choices=[0, 1],
                     help="per-block activation recompute: only block inputs stay saved (long sequences, e.g. "
                          "Llama-3-8B at --seq 32768 on one GPU; ~1/3 more FLOPs)")
-    ap.add_argument("--wgrad-stream", default="auto", choices=["auto", "on", "off"],
-                    help="weight-gradient GEMMs on a second HIP stream beside the data-gradient chain "
-                         "(auto: models narrower than 2048, where it measured +8 %% on GPT-2-small)")
+    ap.add_argument("--wgrad-stream", default="off", choices=["auto", "on", "off"],
+                    help="weight-gradient GEMMs on a second HIP stream beside the data-gradient chain, one rank only "
+                         "(auto: models narrower than 2048, +8 %% on GPT-2-small). Off by default: the one-GPU "
+                         "multi-process rehearsal showed sporadic divergence with it (profiles/r2_experiments.md)")
     ap.add_argument("--grad-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="gradient buffer precision (fp32: accumulation and DP reduction in fp32)")
     ap.add_argument("--cuda-graph", type=int, default=0, choices=[0, 1],

@@ -10,6 +10,17 @@ cross-entropy over the full 128,256 vocabulary and backward (gradients accumulat
 bucketed RCCL gradient collectives overlapped with the last backward (N > 1; ZeRO-1 by default), gradient
 clipping and the fused AdamW update of all 8.03 B parameters. Weights are random-init, tokens synthetic (no
 network / datasets).
+
+Launch: under torchrun (WORLD_SIZE set) every process is one rank. ``--gpus N > 1`` WITHOUT torchrun starts the
+N ranks itself: ``python -m torch.distributed.run`` as a CHILD process (before this process imports torch or
+touches a GPU; never an exec), whose rank 0 prints the JSON line; the exit code is the child's. A collective that
+hangs fails the run after ``--comm-timeout`` seconds (RCCL watchdog abort) instead of burning the lease.
+
+Communication evidence in the JSON (N > 1): ``backend``, ``rccl_world`` (``dist.get_world_size()``),
+``grad_comm_bytes_per_step`` / ``param_gather_bytes_per_step`` (bytes each rank hands to the gradient
+reduce-scatter or all-reduce / the ZeRO-1 all-gather per optimizer step) and ``exposed_comm_ms`` (per step, max
+over ranks): the compute stream's stall between backward's last kernel and the completion of the last gradient
+collective, plus its stalls on ZeRO-1 all-gather gates in the next forward -- CUDA-event timed on the GPU.
 """
 from __future__ import annotations
 
@@ -22,6 +33,29 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _self_launch(n: int) -> int:
+    """N ranks on this node via torchrun in a child process; stdout / stderr pass straight through (rank 0's
+    JSON line included). Nothing here imports torch's CUDA runtime or touches a GPU."""
+    import subprocess
+
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL peer buffers)
+    env.setdefault("OMP_NUM_THREADS", "8")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] --gpus {n} without torchrun: launching {n} ranks ({' '.join(cmd[1:6])} ...)", file=sys.stderr,
+          flush=True)
+    return subprocess.call(cmd, env=env)
 
 
 def main() -> int:
@@ -51,10 +85,9 @@ def main() -> int:
     ap.add_argument("--recompute", type=int, default=0, choices=[0, 1],
                     help="per-block activation recompute: only block inputs stay saved (long sequences, e.g. "
                          "Llama-3-8B at --seq 32768 on one GPU; ~1/3 more FLOPs)")
-    ap.add_argument("--wgrad-stream", default="off", choices=["auto", "on", "off"],
-                    help="weight-gradient GEMMs on a second HIP stream beside the data-gradient chain, one rank only "
-                         "(auto: models narrower than 2048, +8 %% on GPT-2-small). Off by default: the one-GPU "
-                         "multi-process rehearsal showed sporadic divergence with it (profiles/r2_experiments.md)")
+    ap.add_argument("--wgrad-stream", default="auto", choices=["auto", "on", "off"],
+                    help="weight-gradient GEMMs on a second HIP stream beside the data-gradient chain (auto: models "
+                         "narrower than 2048, +8 %% on GPT-2-small; single-rank jobs unless KOP_WGRAD_STREAM_MULTI=1)")
     ap.add_argument("--grad-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="gradient buffer precision (fp32: accumulation and DP reduction in fp32)")
     ap.add_argument("--cuda-graph", type=int, default=0, choices=[0, 1],
@@ -68,7 +101,14 @@ def main() -> int:
     ap.add_argument("--layers", type=int, default=0,
                     help="override the model's layer count (shape rehearsals of big models on one GPU; recorded in "
                          "the JSON config; never used for the headline)")
+    ap.add_argument("--comm-timeout", type=int, default=300,
+                    help="seconds before a hung collective aborts the run (RCCL watchdog; non-zero exit)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return _self_launch(args.gpus)
+    # a collective timeout tears the process group down and aborts the rank (non-zero exit, torchrun stops the rest)
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
 
     import torch
 
@@ -76,16 +116,19 @@ def main() -> int:
     from kubeoperator_amd.models import get_config
     from kubeoperator_amd.train import SyntheticTokens, TrainConfig, Trainer
 
-    info = init_distributed(args.device)
+    info = init_distributed(args.device, timeout_s=args.comm_timeout)
     if args.dp == "auto":
         args.dp = "zero1" if info.world > 1 else "allreduce"
     from kubeoperator_amd.train import gemm_tuning
 
     tuning = gemm_tuning.setup(args.gemm_tuning, rank=info.rank)
     world = info.world
-    if world != args.gpus and info.is_main:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}; reporting the real world size",
-              file=sys.stderr)
+    if world != args.gpus:
+        # launched by torchrun with another rank count than --gpus: never report a different job than was asked for
+        if info.is_main:
+            print(f"[bench] error: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        shutdown(info)
+        return 2
     tc = TrainConfig(model=args.model, micro_batch=args.mbs, seq_len=args.seq, grad_accum=args.accum,
                      dp_mode=args.dp, bucket_mb=args.bucket_mb, warmup_steps=10, total_steps=1000,
                      overlap_optimizer=bool(args.overlap_opt),
@@ -109,6 +152,10 @@ def main() -> int:
     sync()
     barrier(info)
     sync()
+    timing = cuda and world > 1
+    if timing:  # exposed-communication events (a handful per step, no host synchronisation)
+        trainer.dp.finish_waits, trainer.store.gate_waits = [], []
+    comm0, gather0 = trainer.dp.comm_bytes, trainer.dp.gather_bytes
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = trainer.train_step(data.batches(args.accum))
@@ -117,6 +164,15 @@ def main() -> int:
     sync()
     elapsed = time.perf_counter() - t0
     elapsed = all_reduce_max(elapsed, info)
+    exposed_ms = None
+    if timing:
+        trainer.store.await_all()  # the next step's gates: their waits belong to the timed steps' collectives
+        sync()
+        waits = trainer.dp.finish_waits + trainer.store.gate_waits
+        exposed_ms = all_reduce_max(sum(a.elapsed_time(b) for a, b in waits) / args.steps, info)
+        trainer.dp.finish_waits = trainer.store.gate_waits = None
+    comm_step = (trainer.dp.comm_bytes - comm0) // max(1, args.steps)
+    gather_step = (trainer.dp.gather_bytes - gather0) // max(1, args.steps)
     gemm_tuning.finish(tuning, info.rank)
     last_loss = float(loss.item()) if loss is not None else float("nan")
     tokens = trainer.job_tokens_per_step * args.steps
@@ -166,10 +222,21 @@ def main() -> int:
             "peak_mem_gb_rank0": round(mem_gb, 1),
             "setup_s": round(trainer.setup_seconds, 1),
             "gemm_selection": tuning,
+            "backend": info.backend,
+            "rccl_world": _dist_world(),
+            "grad_comm_bytes_per_step": int(comm_step),
+            "param_gather_bytes_per_step": int(gather_step),
+            "exposed_comm_ms": round(exposed_ms, 3) if exposed_ms is not None else None,
         }
         print(json.dumps(out), flush=True)
     shutdown(info)
     return 0
+
+
+def _dist_world() -> int:
+    import torch.distributed as dist
+
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
 if __name__ == "__main__":

@@ -173,15 +173,16 @@ def ldap_authenticate(username: str, password: str) -> M.User:
         "user": escape_filter_value(username)}
     try:
         with _ldap_service_conn(st) as conn:
-            found = None
+            hits = []
             for base in (st.get("AUTH_LDAP_SEARCH_OU") or "").split("|"):
                 if base.strip():
-                    hits = conn.search(base.strip(), flt, attributes=[amap.get("email", "mail")], size_limit=2)
-                    if hits:
-                        found = hits[0]
-                        break
-        if found is None:
+                    hits += conn.search(base.strip(), flt, attributes=[amap.get("email", "mail")], size_limit=2)
+        if not hits:
             raise AuthError("LDAP user not found")
+        if len({h["dn"].lower() for h in hits}) > 1:
+            # ambiguous search (several entries over the bases): never bind as whichever the server lists first
+            raise AuthError("LDAP search matched more than one entry")
+        found = hits[0]
         with LDAPConnection(st["AUTH_LDAP_SERVER_URI"]) as user_conn:
             user_conn.bind(found["dn"], password)
     except LDAPError as e:

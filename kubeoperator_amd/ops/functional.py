@@ -34,11 +34,27 @@ def _lib():
 # Weight gradients on a second HIP stream: the backward's critical path is the data-gradient chain (dX feeds
 # the next layer); the weight-gradient GEMMs (and their operand transposes) only feed the flat gradient buffer.
 # Issued on the store's side stream, they run beside the next layer's kernels instead of between them.
-# ``inputs`` are the tensors ``produce`` reads: recorded on the side stream so the caching allocator does not
-# hand their memory out before it has run. Measured on one MI355X (profiles/r2_wgrad_stream_ab.log): GPT-2-small
-# +8 % (its 768-wide GEMMs leave the chip partly idle), Llama-3-8B -30..-50 % (two full-chip stream-K GEMMs
-# contend), so the trainer enables it per parameter store for narrow models only (``FlatParamStore.wgrad_stream``;
-# ``KOP_WGRAD_STREAM=0/1`` forces it).
+# ``inputs`` are the tensors ``produce`` reads. Two hazards follow from reading them on another stream:
+#
+# * memory reuse: recorded on the side stream (``record_stream``) so the caching allocator does not hand their
+#   memory out before the side stream has run;
+# * in-place accumulation by autograd: when a gradient tensor reaches a node that already holds another
+#   contribution for the same input, autograd adds the two IN PLACE into whichever buffer it holds the last
+#   reference to (``InputBuffer::accumulate``, ``can_accumulate_inplace``). The residual stream makes that
+#   happen: block 0's first norm reads the embedding output ``x`` and passes it on as the residual ``x1``, so
+#   ``x`` gets two gradients -- the second norm's (which is also the ``dY`` of the Wo / proj projection) and the
+#   first norm's. With the side stream lagging, ``dY += dX1`` ran on the compute stream before the side stream's
+#   dW_o read ``dY``, so Wo of layer 0 received the gradient of dY + dX1 (the round-2 divergence: rel. error 0.29,
+#   identical across runs). The store keeps a reference to every input until the side stream has passed it
+#   (``FlatParamStore.hold_side``), which makes autograd allocate a fresh sum instead of writing into it.
+#
+# Measured on one MI355X (profiles/r2_wgrad_stream_ab.log): GPT-2-small +8 % (its 768-wide GEMMs leave the chip
+# partly idle), Llama-3-8B -30..-50 % (two full-chip stream-K GEMMs contend), so the trainer enables it per
+# parameter store for narrow models only (``FlatParamStore.wgrad_stream``; ``KOP_WGRAD_STREAM=0/1`` forces it).
+
+# test hook: GPU cycles of ``torch.cuda._sleep`` enqueued on the side stream before every weight gradient, so the
+# side stream deterministically lags the compute stream (tests/test_wgrad_stream_gpu.py)
+SIDE_LAG_CYCLES = int(os.environ.get("KOP_SIDE_LAG_CYCLES", "0"))
 
 
 def _sink(w: torch.Tensor, produce, *inputs):
@@ -51,12 +67,16 @@ def _sink(w: torch.Tensor, produce, *inputs):
     hooks = w._kop_hooks
     acc = hooks.accumulate_for(w)
     if hooks.store.wgrad_stream and mg.is_cuda and not torch.cuda.is_current_stream_capturing():
-        side = hooks.store.side_stream()
+        store = hooks.store
+        side = store.side_stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
+            if SIDE_LAG_CYCLES > 0:
+                torch.cuda._sleep(SIDE_LAG_CYCLES)
             produce(mg, acc)
         for t in inputs:
             t.record_stream(side)
+        store.hold_side(inputs)
     else:
         produce(mg, acc)
     hooks.ready(w)

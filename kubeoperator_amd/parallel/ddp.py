@@ -22,6 +22,7 @@ stream; ``ProcessGroupNCCL`` orders them after the producing GEMMs on the comput
 """
 from __future__ import annotations
 
+import torch
 import torch.distributed as dist
 
 from ..ops.optim import Segment
@@ -51,7 +52,9 @@ class DataParallel:
         self.sync = True
         self._works = []
         self._gather_works = []
-        self.comm_bytes = 0
+        self.comm_bytes = 0  # gradient bytes handed to collectives (per rank, cumulative)
+        self.gather_bytes = 0  # ZeRO-1 all-gather output bytes (per rank, cumulative)
+        self.finish_waits: list | None = None  # (event, event) around finish_grads (exposed comm timing)
         store.on_ready = self._on_ready
         self.overlapped = False  # set once the optimizer publishes ZeRO-1 gathers itself
 
@@ -79,9 +82,18 @@ class DataParallel:
             self._works.append(dist.reduce_scatter_tensor(self.store.grads[a:e], g, group=group, async_op=True))
 
     def finish_grads(self) -> None:
-        """Make the current (compute) stream wait for every outstanding gradient collective."""
+        """Make the current (compute) stream wait for every outstanding gradient collective. With
+        ``finish_waits`` set (bench.py, GPU), the wait is bracketed by two timing events on the compute stream:
+        backward's last kernel has run at the first, the last collective has completed at the second."""
+        timed = self.finish_waits is not None and self._works and self.store.params.is_cuda
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         for w in self._works:
             w.wait()
+        if timed:
+            e1.record()
+            self.finish_waits.append((e0, e1))
         self._works.clear()
 
     @property
@@ -126,6 +138,7 @@ class DataParallel:
         ``copy_`` at ``wait()``, i.e. mid-forward when the gate is resolved). The ordering that matters --
         bucket Y written before any kernel reads it -- is the gate's stream dependency, not autograd's."""
         pd = self.store.params.data
+        self.gather_bytes += (b.end - b.start) * pd.element_size()
         return dist.all_gather_into_tensor(pd[b.start:b.end], pd[a:e], group=group, async_op=async_op)
 
     def norm_allreduce(self):

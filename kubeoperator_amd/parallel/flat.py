@@ -155,6 +155,8 @@ class FlatParamStore:
         self.use_order: list[int] = []  # bucket indices in the order the forward pass first reads them
         self._used: set[int] = set()
         self._side = None  # weight-gradient stream (ops.functional._sink)
+        self._held: list = []  # (event, tensors) the side stream still reads (hold_side)
+        self.gate_waits: list | None = None  # (event, event) around collective-gate waits (exposed comm timing)
         self.wgrad_stream = False  # issue weight gradients on it (set by the trainer)
         name_to_bucket = {nm: b for b in self.buckets for nm in b.names}
         for s in specs:
@@ -246,10 +248,23 @@ class FlatParamStore:
             self._side = torch.cuda.Stream(device=self.device)
         return self._side
 
+    def hold_side(self, tensors) -> None:
+        """Keep references to tensors the side stream reads until it has passed them (see ops.functional._sink:
+        a tensor autograd holds the only reference to may be accumulated into IN PLACE on the compute stream).
+        Entries whose event has completed are dropped on the way (host-side query, no synchronisation)."""
+        ev = torch.cuda.Event()
+        ev.record(self._side)
+        held = self._held
+        while held and held[0][0].query():
+            held.pop(0)
+        held.append((ev, tuple(tensors)))
+
     def join_side(self) -> None:
-        """The compute stream waits for every weight gradient issued on the side stream (end of backward)."""
+        """The compute stream waits for every weight gradient issued on the side stream (end of backward);
+        from here on every compute-stream write is ordered after the side stream's reads."""
         if self._side is not None:
             torch.cuda.current_stream().wait_stream(self._side)
+        self._held.clear()
 
     # forward gates ------------------------------------------------------------------------------
     def await_param(self, p) -> None:
@@ -262,7 +277,7 @@ class FlatParamStore:
             self.use_order.append(b.index)
         g = self.gates.pop(b.index, None)
         if g is not None:
-            _resolve(g)
+            self._resolve_timed(g)
 
     def set_gate(self, index: int, gate) -> None:
         self.gates[index] = gate
@@ -270,7 +285,19 @@ class FlatParamStore:
     def await_all(self) -> None:
         """Resolve every outstanding gate (before checkpointing, evaluation, or the next optimizer step)."""
         for i in list(self.gates):
-            _resolve(self.gates.pop(i))
+            self._resolve_timed(self.gates.pop(i))
+
+    def _resolve_timed(self, gate) -> None:
+        """Resolve a gate; with ``gate_waits`` set (bench.py), a collective gate (ZeRO-1 all-gather) is bracketed by
+        two timing events on the compute stream: their distance is the time the compute stream stalled on it."""
+        if self.gate_waits is None or isinstance(gate, torch.cuda.Event):
+            _resolve(gate)
+            return
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _resolve(gate)
+        e1.record()
+        self.gate_waits.append((e0, e1))
 
     # transposed weight copies (data-gradient GEMMs) ----------------------------------------------
     def enable_transposed(self, min_width: int = 2048) -> int:

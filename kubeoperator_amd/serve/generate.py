@@ -122,8 +122,13 @@ class LlamaGenerator:
             else:
                 qkv = ref.rope_ref(qkv, self.cos, self.sin, S, Hq + Hkv, D)
             q, k, v = qkv[:, :a], qkv[:, a:kc], qkv[:, kc:]
-            self.cache.k[i][rows, :, :S].copy_(k.reshape(B, S, Hkv, D).transpose(1, 2))
-            self.cache.v[i][rows, :, :S].copy_(v.reshape(B, S, Hkv, D).transpose(1, 2))
+            kh, vh = k.reshape(B, S, Hkv, D).transpose(1, 2), v.reshape(B, S, Hkv, D).transpose(1, 2)
+            if contiguous:  # a slice of the cache: copy in place
+                self.cache.k[i][rows, :, :S].copy_(kh)
+                self.cache.v[i][rows, :, :S].copy_(vh)
+            else:  # index tensor: advanced indexing returns a COPY, so write through index_put_ (assignment)
+                self.cache.k[i][rows, :, :S] = kh
+                self.cache.v[i][rows, :, :S] = vh
             if q.is_cuda and S % 128 == 0:  # the HIP flash forward's tile constraint
                 o, _ = kf.flash_attention(q, k, v, B, S, Hq, Hkv, D, causal=True, scale=self.scale)
             else:

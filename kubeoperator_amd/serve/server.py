@@ -186,8 +186,24 @@ def load_model(name: str, device: str, ckpt: str = ""):
     if ckpt:
         from ..train import checkpoint
 
+        import os
+
         step = checkpoint.latest_step(ckpt)
+        if step is None:
+            tp_trees = [d for d in os.listdir(ckpt) if d.startswith("tp")] if os.path.isdir(ckpt) else []
+            if tp_trees:
+                raise ValueError(f"{ckpt} holds tensor-parallel checkpoint trees ({', '.join(sorted(tp_trees))}): "
+                                 "the server loads single-GPU (tp 1) checkpoints")
+            raise ValueError(f"{ckpt} holds no complete checkpoint (no 'latest' marker)")
         sd = torch.load(f"{ckpt}/step_{step}/rank_0.pt", map_location=device, weights_only=True)
+        if int(sd.get("tp", 1)) != 1:
+            raise ValueError(f"checkpoint {ckpt} step {step} is a tensor-parallel shard (tp {sd['tp']})")
+        mc = sd.get("model_config") or {}
+        want = cfg.to_dict()
+        diff = {k: (mc[k], want[k]) for k in ("arch", "vocab_size", "hidden", "n_layers", "n_heads", "n_kv_heads",
+                                              "ffn_hidden", "tie_embeddings") if k in mc and mc[k] != want[k]}
+        if diff:
+            raise ValueError(f"checkpoint model_config differs from --model {name}: {diff}")
         flat, lay = sd["params"], sd["layout"]
         named = dict(m.named_parameters())
         with torch.no_grad():

@@ -50,6 +50,11 @@ def save(trainer, directory: str, info: DistInfo) -> str:
     os.replace(tmp, path)
     barrier(info)
     if info.is_main:
+        # a step directory may hold files of an earlier, crashed attempt at a larger world size (same step number,
+        # another trajectory): drop every rank file past this world before the step becomes "latest"
+        for f in os.listdir(d):
+            if f.startswith("rank_") and f.endswith(".pt") and int(f[5:-3]) >= info.world:
+                os.remove(os.path.join(d, f))
         with open(os.path.join(directory, "latest.tmp"), "w") as f:
             f.write(str(step))
         os.replace(os.path.join(directory, "latest.tmp"), os.path.join(directory, "latest"))
@@ -65,9 +70,13 @@ def latest_step(directory: str):
         return int(f.read().strip())
 
 
-def _files(d: str) -> list[str]:
-    ranks = sorted(int(f[5:-3]) for f in os.listdir(d) if f.startswith("rank_") and f.endswith(".pt"))
-    return [os.path.join(d, f"rank_{r}.pt") for r in ranks]
+def _files(d: str, world: int) -> list[str]:
+    """The rank files of a step written at ``world`` ranks: exactly rank_0 .. rank_{world-1}."""
+    paths = [os.path.join(d, f"rank_{r}.pt") for r in range(world)]
+    missing = [p for p in paths if not os.path.exists(p)]
+    if missing:
+        raise ValueError(f"incomplete checkpoint {d}: missing {[os.path.basename(p) for p in missing]}")
+    return paths
 
 
 def load(trainer, directory: str, info: DistInfo, step: int | None = None) -> int | None:
@@ -85,9 +94,11 @@ def load(trainer, directory: str, info: DistInfo, step: int | None = None) -> in
     if step is None:
         return None
     d = os.path.join(directory, f"step_{step}")
-    files = _files(d)
+    head = torch.load(os.path.join(d, "rank_0.pt"), map_location="cpu", weights_only=True, mmap=True)
+    files = _files(d, int(head["world"]))
     own = os.path.join(d, f"rank_{info.rank}.pt")
-    head = torch.load(files[0], map_location="cpu", weights_only=True, mmap=True)
+    if info.rank >= int(head["world"]):
+        own = files[0]  # a rank the writing job did not have: reshards from the others
     if getattr(getattr(trainer, "tp", None), "seq_parallel", False) and head["world"] != info.world:
         raise ValueError("a sequence-parallel checkpoint resumes on the topology that wrote it")
     if "layout" in head:  # identical flat layout (world size AND bucket boundaries): plain copy
@@ -143,6 +154,9 @@ def _reshard(trainer, head: dict, files: list[str]) -> None:
     new_starts = [x[0] for x in new_p]
     for f in files:
         sd = head if f == files[0] else torch.load(f, map_location="cpu", weights_only=True, mmap=True)
+        if int(sd["world"]) != int(head["world"]) or int(sd["step"]) != int(head["step"]):
+            raise ValueError(f"{f} belongs to another save (world {sd['world']}, step {sd['step']}) than rank_0's "
+                             f"(world {head['world']}, step {head['step']})")
         osd = sd["optimizer"]
         old_p = sorted(sd["layout"]["pieces"])
         old_starts = [x[0] for x in old_p]

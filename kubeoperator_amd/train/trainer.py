@@ -43,9 +43,8 @@ class TrainConfig:
     grad_dtype: str = "bf16"  # bf16 | fp32: gradient buffer (micro-batch accumulation + DP reduction) precision
     fp8: bool = False  # E4M3 forward + data-gradient GEMMs of the block projections (ops/fp8.py; opt-in)
     recompute: bool = False  # per-block activation recompute (long sequences: only block inputs stay saved)
-    # weight-gradient GEMMs on a side stream (one rank): auto (narrow models, hidden < 2048) | on | off. Off by
-    # default: a contended-GPU rehearsal showed sporadic divergence with it (profiles/r2_experiments.md)
-    wgrad_stream: str = "off"
+    # weight-gradient GEMMs on a side stream: auto (narrow models, hidden < 2048) | on | off
+    wgrad_stream: str = "auto"
     tp: int = 1  # tensor-parallel degree (Llama; TP groups of consecutive ranks, DP across them: parallel.tensor)
     sp: bool = False  # sequence parallelism on top of TP (norms, residual stream, LM head on 1/tp of the rows)
     seed: int = 1234
@@ -105,11 +104,9 @@ class Trainer:
         env = os.environ.get("KOP_WGRAD_STREAM")
         want = (tc.wgrad_stream == "on" or (tc.wgrad_stream == "auto" and self.cfg.hidden < 2048)) \
             if env not in ("0", "1") else env == "1"
-        # one data-parallel rank only: with ZeRO-1 gradient collectives issued from the side stream, the
-        # 4-rank rehearsal on one MI355X diverged from the single-process update (rel. error 0.04-0.19 vs
-        # 0.008 with the side stream off; profiles/r2_dp_wgrad_stream_ab.log) -- multi-rank jobs keep the
-        # weight gradients on the compute stream
-        if want and self.dp_info.world > 1:
+        # multi-rank jobs (data or tensor parallel) only with KOP_WGRAD_STREAM_MULTI=1 until the one-GPU
+        # multi-rank rehearsal confirms the in-place-accumulation fix (ops.functional._sink) there as well
+        if want and info.world > 1 and os.environ.get("KOP_WGRAD_STREAM_MULTI") != "1":
             if tc.wgrad_stream == "on" or env == "1":
                 raise ValueError("the weight-gradient side stream is single-rank only (wgrad_stream on, world > 1)")
             want = False

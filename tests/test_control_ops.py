@@ -591,3 +591,25 @@ def test_ldap_login_and_sync_with_builtin_client(control):
             assert s.query(M.User).filter_by(username="bob", source="ldap").count() == 1
     finally:
         srv.close()
+
+
+def test_ldap_login_refuses_an_ambiguous_search(control):
+    """Two entries match the user name (one per search base): the login is refused rather than binding as
+    whichever DN the server returns first (django-auth-ldap behaviour, which the reference builds on)."""
+    from kubeoperator_amd.control.domain import context, users
+
+    srv = _ldap_server({
+        "cn=admin,dc=ex,dc=org": {"_pw": "adminpw"},
+        "uid=carol,ou=people,dc=ex,dc=org": {"_pw": "pw1", "uid": ["carol"], "objectClass": ["person"]},
+        "uid=carol,ou=staff,dc=ex,dc=org": {"_pw": "pw2", "uid": ["carol"], "objectClass": ["person"]},
+    })
+    try:
+        context.set_settings({"AUTH_LDAP_ENABLE": "true", "AUTH_LDAP_SERVER_URI": f"ldap://127.0.0.1:{srv.getsockname()[1]}",
+                              "AUTH_LDAP_BIND_DN": "cn=admin,dc=ex,dc=org", "AUTH_LDAP_BIND_PASSWORD": "adminpw",
+                              "AUTH_LDAP_SEARCH_OU": "ou=people,dc=ex,dc=org|ou=staff,dc=ex,dc=org",
+                              "AUTH_LDAP_SEARCH_FILTER": "(uid=%(user)s)"}, tab="ldap")
+        for pw in ("pw1", "pw2"):
+            with pytest.raises(users.AuthError, match="more than one"):
+                users.authenticate("carol", pw)
+    finally:
+        srv.close()

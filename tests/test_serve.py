@@ -174,3 +174,47 @@ def test_continuous_batching_matches_independent_generation(max_seq):
     b.close()
     assert got == want
     assert b.steps > 0 and b.gen.cache.max_len == 0
+
+
+def test_prefill_into_non_contiguous_slots_matches_independent_generation():
+    """Slots [0, 2] of a 3-slot cache (slot 1 busy): the index-tensor write must reach the cache -- decode from
+    those slots must match each prompt generated alone."""
+    m = _model("cpu")
+    ids = torch.randint(0, m.cfg.vocab_size, (2, 12), generator=torch.Generator().manual_seed(4))
+    gen = LlamaGenerator(m, max_batch=3, max_seq=24)
+    logits = gen.prefill(ids, slots=[0, 2])
+    assert gen.cache.k[0][1].abs().sum() == 0  # the busy slot is untouched
+    for b, slot in enumerate((0, 2)):
+        assert gen.cache.k[0][slot, :, :12].abs().sum() > 0
+        alone = LlamaGenerator(m, max_batch=1, max_seq=24)
+        ref_logits = alone.prefill(ids[b:b + 1])
+        assert torch.allclose(logits[b], ref_logits[0], atol=1e-3)
+        # one decode step from the slot: attends over the prefilled K/V, so it must match the lone generator
+        tok = ref_logits.argmax(-1)
+        full = torch.zeros(3, dtype=torch.long)
+        full[slot] = tok[0]
+        active = [r == slot for r in range(3)]
+        step = gen.decode(full, active=active)
+        exp = alone.decode(tok)
+        err = (step[slot] - exp[0]).abs().max().item() / exp.abs().max().item()
+        assert err < 1e-2, err
+
+
+def test_serving_load_model_refuses_unusable_checkpoints(tmp_path):
+    """Empty directory, tensor-parallel trees, or a checkpoint of another model: a clear error, not a KeyError
+    on ``step_None`` or a shape mismatch mid-copy."""
+    from kubeoperator_amd.parallel.dist import DistInfo
+    from kubeoperator_amd.serve.server import load_model
+    from kubeoperator_amd.train import TrainConfig, Trainer, checkpoint
+
+    with pytest.raises(ValueError, match="no complete checkpoint"):
+        load_model("tiny_llama", "cpu", str(tmp_path))
+    (tmp_path / "tp0_of2").mkdir()
+    with pytest.raises(ValueError, match="tensor-parallel"):
+        load_model("tiny_llama", "cpu", str(tmp_path))
+    ck = tmp_path / "ck"
+    tr = Trainer(TrainConfig(model="tiny_llama", micro_batch=1, seq_len=32), DistInfo())
+    checkpoint.save(tr, str(ck), DistInfo())
+    assert load_model("tiny_llama", "cpu", str(ck)) is not None
+    with pytest.raises(ValueError, match="model_config differs"):
+        load_model("llama3_1b_proxy", "cpu", str(ck))

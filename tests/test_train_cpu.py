@@ -310,6 +310,34 @@ def test_checkpoint_reshards_across_world_sizes(tmp_path):
     assert torch.equal(before, _run_elastic(4, tmp_path, "e", ckpt_in=c4))
 
 
+def test_checkpoint_ignores_stale_rank_files_of_another_attempt(tmp_path):
+    """A step directory can hold rank files of a crashed attempt at a larger world size (same step number,
+    another trajectory): save removes them, and load reads exactly rank_0 .. rank_{world-1} of rank_0's save."""
+    a = Trainer(_tc(seed=1), DistInfo())
+    b = Trainer(_tc(seed=2), DistInfo())
+    for s in range(2):
+        a.train_step([_batch(a, seed=s)])
+        b.train_step([_batch(b, seed=s + 10)])
+    d = tmp_path / "step_2"
+    d.mkdir()
+    stale = b.state_dict()
+    stale["world"] = 4
+    torch.save(stale, d / "rank_3.pt")  # left behind by a world-4 attempt that crashed before "latest"
+    checkpoint.save(a, str(tmp_path), DistInfo())
+    assert sorted(os.listdir(d)) == ["rank_0.pt"]
+    torch.save(stale, d / "rank_1.pt")  # appears after the save: never read for a world-1 checkpoint
+    c = Trainer(_tc(seed=3), DistInfo())
+    assert checkpoint.load(c, str(tmp_path), DistInfo()) == 2
+    assert torch.equal(c.store.params, a.store.params)
+    assert torch.equal(c.opt.exp_avg, a.opt.exp_avg)
+    # a world-2 save whose rank_1 belongs to another save is refused instead of silently mixed in
+    head = torch.load(d / "rank_0.pt", weights_only=True)
+    head["world"] = 2
+    torch.save(head, d / "rank_0.pt")
+    with pytest.raises(ValueError, match="another save"):
+        checkpoint.load(Trainer(_tc(seed=4, bucket_mb=0), DistInfo()), str(tmp_path), DistInfo())
+
+
 def test_checkpoint_reshards_when_bucket_layout_changes(tmp_path):
     """Same world size, different bucket size: the optimizer-state segments move, so the loader must reshard
     by parameter instead of copying the flat state buffers."""

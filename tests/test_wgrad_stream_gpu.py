@@ -1,0 +1,61 @@
+"""Weight-gradient side stream (ops.functional._sink) under a forced lag.
+
+``SIDE_LAG_CYCLES`` enqueues a ``torch.cuda._sleep`` on the side stream before every weight gradient, so the side
+stream always runs behind the compute stream -- the worst case of a contended GPU, made deterministic. Three
+optimizer steps with the side stream on must then match the same steps on one stream. A second test removes the
+reference holding of ``FlatParamStore.hold_side`` and checks that the lag reproduces the round-2 divergence
+(autograd accumulating the block-0 residual gradient in place into the Wo / proj dY the side stream still reads).
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+LAG = 1_000_000  # GPU clock cycles per weight gradient
+
+
+def _train(model: str, stream: bool, accum: int, monkeypatch, hold: bool = True):
+    from kubeoperator_amd.ops import functional
+    from kubeoperator_amd.parallel.dist import DistInfo
+    from kubeoperator_amd.parallel.flat import FlatParamStore
+    from kubeoperator_amd.train import TrainConfig, Trainer
+
+    monkeypatch.setenv("KOP_WGRAD_STREAM", "1" if stream else "0")
+    monkeypatch.setattr(functional, "SIDE_LAG_CYCLES", LAG if stream else 0)
+    if not hold:
+        monkeypatch.setattr(FlatParamStore, "hold_side", lambda self, tensors: None)
+    # clipping off: the grad-norm sum uses float atomics, the rest of the step is deterministic
+    tr = Trainer(TrainConfig(model=model, micro_batch=4, seq_len=256, grad_accum=accum, lr=1e-2, warmup_steps=1,
+                             total_steps=10, bucket_mb=1, grad_clip=0.0),
+                 DistInfo(0, 0, 1, "none", torch.device("cuda", 0)))
+    assert tr.store.wgrad_stream == stream
+    init = tr.store.params.detach().float().clone()
+    for step in range(3):
+        g = torch.Generator().manual_seed(100 + step)
+        mbs = []
+        for _ in range(accum):
+            ids = torch.randint(0, tr.cfg.vocab_size, (4, 257), generator=g)
+            mbs.append((ids[:, :-1].cuda(), ids[:, 1:].cuda()))
+        tr.train_step(mbs)
+    tr.store.await_all()
+    torch.cuda.synchronize()
+    monkeypatch.undo()
+    return init, tr.store.params.detach().float()
+
+
+@pytest.mark.parametrize("model", ["tiny_llama", "tiny_gpt2"])
+@pytest.mark.parametrize("accum", [1, 4])
+def test_lagging_side_stream_matches_one_stream(model, accum, monkeypatch):
+    init, off = _train(model, False, accum, monkeypatch)
+    _, on = _train(model, True, accum, monkeypatch)
+    rel = ((on - off).norm() / (off - init).norm()).item()
+    assert rel < 5e-3, rel
+
+
+def test_lag_without_reference_hold_reproduces_divergence(monkeypatch):
+    """Documents the root cause: without ``hold_side`` the in-place residual-gradient accumulation races the
+    lagging side stream and layer 0's Wo gradient is wrong."""
+    init, off = _train("tiny_llama", False, 1, monkeypatch)
+    _, on = _train("tiny_llama", True, 1, monkeypatch, hold=False)
+    rel = ((on - off).norm() / (off - init).norm()).item()
+    assert rel > 2e-2, rel

@@ -299,10 +299,49 @@ def exit_new_node(cluster_name: str) -> None:
 
 
 # --------------------------------------------------------------------------------------------- execution
+def _storage_vars(c: M.Cluster) -> dict:
+    """Variables of the storage back-end the cluster uses: the NFS server named by ``configs["nfs_storage"]``
+    (its address / export path), or the external Ceph cluster bound to it (monitors, fsid, pool, key; the key
+    stays encrypted at rest and is decrypted here, for the run only)."""
+    out: dict = {}
+    cfg = c.configs or {}
+    with session_scope() as s:
+        if cfg.get("nfs_storage"):
+            n = s.scalar(select(M.NfsStorage).where(M.NfsStorage.name == cfg["nfs_storage"]))
+            if n is None:
+                raise NotFound(f"nfs storage {cfg['nfs_storage']} not found")
+            v = n.vars or {}
+            out.update({k: v[k] for k in ("storage_nfs_server", "storage_nfs_server_path") if k in v})
+        b = s.scalar(select(M.ClusterCephStorage).where(M.ClusterCephStorage.cluster_id == c.id))
+        if b is not None:
+            v = dict(s.get(M.CephStorage, b.storage_id).vars or {})
+            if v.get("ceph_key"):
+                try:
+                    v["ceph_key"] = context.dec(v["ceph_key"])
+                except Exception:
+                    pass  # stored in clear by an older record
+            out.update(v)
+    return out
+
+
+def _cloud_vars(c: M.Cluster) -> dict:
+    """AUTOMATIC clusters: the plan's region / zone variables (vCenter or OpenStack endpoint and credentials,
+    datastores / volume types) for the vSphere and Cinder storage roles -- resolved per run, never copied into
+    the stored cluster configs."""
+    if not c.plan_id:
+        return {}
+    from . import cloud
+
+    return cloud.mixed_vars(c.plan_id)
+
+
 def extra_vars(c: M.Cluster) -> dict:
-    """{cluster_name, cluster_domain} + settings + cluster configs (deploy.py:41-47)."""
+    """{cluster_name, cluster_domain} + settings + cloud / storage back-end vars + cluster configs
+    (deploy.py:41-47)."""
     ev = {"cluster_name": c.name, "cluster_domain": c.cluster_doamin_suffix}
     ev.update(context.get_settings())
+    ev.update(_cloud_vars(c))
+    ev.update(_storage_vars(c))
     ev.update(c.configs or {})
     ev.setdefault("base_dir", "/etc/kubeoperator")
     from ..conf import get_config

@@ -75,8 +75,13 @@ def delete_nfs(name: str) -> None:
 
 
 def create_ceph(data: dict) -> dict:
+    """External Ceph cluster (fsid ``ceph_cluster_id``, ``ceph_monitors``, ``ceph_pool``, ``ceph_user``, ``ceph_key``);
+    the key is stored encrypted (store/crypto) and decrypted only into a deploy run's variables."""
+    v = dict(data.get("vars") or {})
+    if v.get("ceph_key"):
+        v["ceph_key"] = context.enc(v["ceph_key"])
     with session_scope() as s:
-        c = M.CephStorage(name=data["name"], vars=dict(data.get("vars") or {}))
+        c = M.CephStorage(name=data["name"], vars=v)
         s.add(c)
         s.flush()
         return c.to_dict()

@@ -38,7 +38,7 @@ from .templating import LazyVars, TemplateError, evaluate, render
 from .transport import FakeTransport, HostConn, Transport, Unreachable
 
 TASK_KEYWORDS = {
-    "name", "when", "loop", "with_items", "with_list", "with_dict", "with_sequence", "loop_control", "register",
+    "name", "when", "loop", "with_items", "with_list", "with_dict", "with_sequence", "with_nested", "loop_control", "register",
     "until", "retries", "delay", "ignore_errors", "failed_when", "changed_when", "delegate_to", "run_once",
     "notify", "tags", "vars", "environment", "become", "become_user", "no_log", "args", "block", "rescue",
     "always", "include_tasks", "import_tasks", "include_role", "import_role", "listen", "check_mode",
@@ -500,8 +500,13 @@ class Runner:
                 spec = t.get("include_role") or t.get("import_role")
                 rn = render(spec["name"] if isinstance(spec, dict) else spec, v)
                 role = self.loader.load_role(rn, base_dir)
+                tasks = role.tasks
+                tf = render(spec.get("tasks_from"), v) if isinstance(spec, dict) and spec.get("tasks_from") else None
+                if tf:  # one task file of the role, with the role's defaults / vars (Ansible tasks_from)
+                    tp = os.path.join(role.path, "tasks", tf if str(tf).endswith((".yml", ".yaml")) else f"{tf}.yml")
+                    tasks = self.loader.expand_tasks(_load_yaml(tp) or [], os.path.dirname(tp), role)
                 inner = []
-                for x in role.tasks:
+                for x in tasks:
                     x = copy.deepcopy(x)
                     x["_role_defaults"] = role.defaults
                     x["_role_vars"] = role.vars
@@ -676,6 +681,11 @@ class Runner:
                         flat.extend(x if isinstance(x, list) else [x])
                     items = flat
                 return list(items or [])
+        if "with_nested" in t:  # cartesian product of the listed lists
+            import itertools
+
+            lists = [x if isinstance(x, list) else [x] for x in (render(t["with_nested"], v) or [])]
+            return [list(p) for p in itertools.product(*lists)] if lists else []
         if "with_dict" in t:
             d = render(t["with_dict"], v) or {}
             return [{"key": k, "value": val} for k, val in d.items()]

@@ -104,6 +104,11 @@ class SimFarm(FakeTransport):
         return sum(1 for h, fs in self.fs.items()
                    if self.is_gpu(h) and "/etc/kubernetes/kubelet.conf" in fs and self.GPU_LABEL in fs)
 
+    def _joined(self, workers_only: bool = False) -> int:
+        """Machines that joined the simulated cluster (kubelet.conf present); workers hold no admin.conf."""
+        return sum(1 for fs in self.fs.values() if "/etc/kubernetes/kubelet.conf" in fs
+                   and not (workers_only and "/etc/kubernetes/admin.conf" in fs))
+
     def _install_rules(self):
         R = self.add_rule
 
@@ -170,14 +175,23 @@ class SimFarm(FakeTransport):
         R(r"kubeadm reset", fn=reset)
         R(r"kubectl get node (\S+) --no-headers",
           fn=lambda h, c, fs: (0, f"{c.split('get node ')[1].split()[0]} Ready worker 1m v1.30.6", ""))
-        R(r"kube-flannel get pods .* wc -l", stdout="0")
-        R(r"calico-node -o jsonpath", stdout="2/2")
-        R(r"deploy coredns -o jsonpath", stdout="2")
-        R(r"deploy chartmuseum -o jsonpath", stdout="1")
+        R(r"get ds \S+ -o jsonpath='\{\.status\.numberReady\}/\{\.status\.desiredNumberScheduled\}'",
+          fn=lambda h, c, fs: (0, f"{self._joined()}/{self._joined()}", ""))
+        R(r"get deploy \S+ -o jsonpath='\{\.status\.readyReplicas\}'", stdout="2")
         R(r"test-sc-pod -o jsonpath", stdout="Succeeded")
+        R(r"is-default-class\}'", stdout="true")
+        R(r"get cephcluster rook-ceph -o jsonpath", stdout="Ready/HEALTH_OK")
+        R(r"-l app=rook-ceph-osd --no-headers -o name \| wc -l", fn=lambda h, c, fs: (0, str(self._joined(True)), ""))
+        R(r"app=rook-ceph-osd-prepare", stdout="Succeeded")
+        R(r"\{\.spec\.providerID\}.*grep -c '\^(vsphere|openstack)://'",
+          fn=lambda h, c, fs: (0, str(self._joined()), ""))
+        R(r"get node \S+ -o jsonpath='\{\.spec\.providerID\}'$", stdout="vsphere://4211aa00-sim")
+        R(r"get node \S+ -o jsonpath='\{\.status\.conditions", stdout="True")
+        R(r"get pv -l kubeoperator\.io/storage=local-volume",
+          fn=lambda h, c, fs: (0, "Available " * self._joined(True), ""))
         R(r"awk '\$2 != \"Ready\"' \| wc -l", stdout="0")
         R(r"/sys/class/kfd/kfd/topology", fn=lambda h, c, fs: (0, str(self.gpus_per_host if self.is_gpu(h) else 0), ""))
-        R(r"rocminfo \| grep -c", fn=lambda h, c, fs: (0, str(self.gpus_per_host if self.is_gpu(h) else 0), ""))
+        R(r"rocminfo \| awk", fn=lambda h, c, fs: (0, str(self.gpus_per_host if self.is_gpu(h) else 0), ""))
         R(r"allocatable\.amd", fn=lambda h, c, fs: (0, " ".join([str(self.gpus_per_host)] * self._n_gpu_nodes()) + " ", ""))
         R(r"app=rocminfo-validate -o jsonpath", fn=lambda h, c, fs: (0, "Succeeded " * self._n_gpu_nodes(), ""))
         R(r"kubectl -n kube-system logs", stdout="Marketing Name: AMD Instinct MI355X\n  Name: gfx950")

@@ -10,6 +10,10 @@
 * ``FakeTransport`` -- a scripted host farm for CI: every command is recorded, answered by the first
   matching rule (regex -> rc/stdout/stderr or callable), files live in an in-memory filesystem per host,
   and faults can be injected (unreachable hosts, failing commands, nth-call failures, latency).
+
+Every command runs under ``bash -o pipefail`` (``SHELL``): a pipeline such as ``kubeadm init ... | tail`` fails
+when ``kubeadm`` fails instead of reporting ``tail``'s status -- Ansible's ``shell`` module (``/bin/sh -c``)
+masks those failures, and the provisioning roles are written for the stricter shell.
 """
 from __future__ import annotations
 
@@ -22,6 +26,10 @@ import tempfile
 import threading
 import time
 from dataclasses import dataclass, field
+
+
+SHELL = ["/bin/bash", "-o", "pipefail", "-c"]
+SHELL_STR = "/bin/bash -o pipefail -c "
 
 
 class Unreachable(Exception):
@@ -96,7 +104,7 @@ class LocalTransport(Transport):
             e.update({k: str(v) for k, v in env.items()})
         if self.root:
             e["KOP_SANDBOX_ROOT"] = self.root
-        p = subprocess.run(["/bin/bash", "-c", cmd], input=stdin, capture_output=True, text=True, timeout=timeout,
+        p = subprocess.run([*SHELL, cmd], input=stdin, capture_output=True, text=True, timeout=timeout,
                            env=e, cwd=self.root or None)
         return CmdResult(p.returncode, p.stdout, p.stderr, time.time() - t0)
 
@@ -194,9 +202,9 @@ class SSHTransport(Transport):
         opts, penv = self._base(conn)
         remote = _env_prefix(env) + cmd
         if conn.become and conn.user != "root":
-            remote = "sudo -H -n /bin/bash -c " + shlex.quote(remote)
+            remote = "sudo -H -n " + SHELL_STR + shlex.quote(remote)
         else:
-            remote = "/bin/bash -c " + shlex.quote(remote)
+            remote = SHELL_STR + shlex.quote(remote)
         argv = [self.ssh_bin, *opts, "-p", str(conn.port), f"{conn.user}@{conn.address}", remote]
         t0 = time.time()
         try:
@@ -213,7 +221,7 @@ class SSHTransport(Transport):
         if mode is not None:
             cmd += f" && chmod {mode:o} {q}"
         opts, penv = self._base(conn)
-        remote = "/bin/bash -c " + shlex.quote(cmd)
+        remote = SHELL_STR + shlex.quote(cmd)
         if conn.become and conn.user != "root":
             remote = "sudo -H -n " + remote
         argv = [self.ssh_bin, *opts, "-p", str(conn.port), f"{conn.user}@{conn.address}", remote]

@@ -642,6 +642,10 @@ class Runner:
         lc = t.get("loop_control", {}) or {}
         loop_var = lc.get("loop_var", "item")
         v0 = self.task_vars(h, t)
+        # conditions inherited from a role / import / block do not depend on the loop item: a task skipped by
+        # them never templates its loop (which may name a variable only its skipped siblings register)
+        if t.get("_when_extra") and not all(evaluate(c, v0) for c in t["_when_extra"]):
+            return {"skipped": True, "changed": False, "msg": "Conditional result was False"}
         items = self._loop_items(t, v0)
         if items is None:
             if not self._when(t, v0):

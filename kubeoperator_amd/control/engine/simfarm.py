@@ -56,6 +56,11 @@ class SimFarm(FakeTransport):
         "/etc/resolv.conf": b"nameserver 127.0.0.53\n",
         "/etc/fstab": b"UUID=0 / ext4 defaults 0 1\n",
         "/etc/exports": b"",
+        "/etc/login.defs": b"MAIL_DIR /var/mail\nPASS_MAX_DAYS\t99999\nPASS_MIN_DAYS\t0\nUMASK\t\t022\n",
+        "/etc/passwd": b"root:x:0:0:root:/root:/bin/bash\ndaemon:x:1:1:daemon:/usr/sbin:/bin/sh\n",
+        "/etc/group": b"root:x:0:\n",
+        "/etc/shadow": b"root:*:19000:0:99999:7:::\n",
+        "/etc/gshadow": b"root:*::\n",
     }
 
     def _seed(self, host: str) -> dict:
@@ -187,6 +192,21 @@ class SimFarm(FakeTransport):
           fn=lambda h, c, fs: (0, str(self._joined()), ""))
         R(r"get node \S+ -o jsonpath='\{\.spec\.providerID\}'$", stdout="vsphere://4211aa00-sim")
         R(r"get node \S+ -o jsonpath='\{\.status\.conditions", stdout="True")
+        R(r"get apprepositories (\S+) -o jsonpath='\{\.metadata\.name\}'",
+          fn=lambda h, c, fs: (0, c.split("get apprepositories ")[1].split()[0], ""))
+        R(r"get ingress \S+ -o name --ignore-not-found",
+          fn=lambda h, c, fs: (0, "ingress.networking.k8s.io/" + c.split("get ingress ")[1].split()[0], ""))
+
+        def f5_annotate(host, cmd, fs):
+            ip = cmd.split("virtual-server.f5.com/ip=", 1)[1].split()[0]
+            fs["/sim/f5-virtual-servers"] = fs.get("/sim/f5-virtual-servers", b"") + ip.encode() + b"\n"
+            return 0, "annotated", ""
+
+        R(r"annotate ingress .*virtual-server\.f5\.com/ip=", fn=f5_annotate)
+        R(r"get ingress -A -o jsonpath=.*loadBalancer",
+          fn=lambda h, c, fs: (0, fs.get("/sim/f5-virtual-servers", b"").decode(), ""))
+        R(r"^sysctl -n net\.ipv4\.ip_forward net\.bridge\.bridge-nf-call-iptables$", stdout="1\n1")
+        R(r"awk -F: '\$3 < \d+ .*/etc/passwd", stdout="daemon\nbin\nsync")
         R(r"get pv -l kubeoperator\.io/storage=local-volume",
           fn=lambda h, c, fs: (0, "Available " * self._joined(True), ""))
         R(r"awk '\$2 != \"Ready\"' \| wc -l", stdout="0")

@@ -272,11 +272,27 @@ class _SandboxedNativeEnvironment(ImmutableSandboxedEnvironment):
 _SandboxedNativeEnvironment.template_class = NativeTemplate
 
 
+class _ChainableStrictUndefined(StrictUndefined):
+    """Strict, but attribute / item access on an undefined value yields another undefined (Ansible's
+    AnsibleUndefined behaviour): ``reg.stdout_lines | default([])`` works when ``reg`` was never registered
+    (its task was skipped), while printing, iterating or comparing an undefined still raises."""
+
+    __slots__ = ()
+
+    def __getattr__(self, name):
+        if name[:2] == "__":
+            raise AttributeError(name)
+        return _ChainableStrictUndefined(name=f"{self._undefined_name}.{name}" if self._undefined_name else name)
+
+    def __getitem__(self, key):
+        return _ChainableStrictUndefined(name=f"{self._undefined_name}[{key!r}]")
+
+
 def _make_env(native: bool):
     # Sandboxed: cluster configs and execution params come from API users (item MANAGERs) and are merged
     # into the variables, so a template must not reach Python internals (attribute walks to globals, etc.).
     cls = _SandboxedNativeEnvironment if native else ImmutableSandboxedEnvironment
-    env = cls(undefined=StrictUndefined, keep_trailing_newline=True, trim_blocks=True, lstrip_blocks=False,
+    env = cls(undefined=_ChainableStrictUndefined, keep_trailing_newline=True, trim_blocks=True, lstrip_blocks=False,
               extensions=["jinja2.ext.do", "jinja2.ext.loopcontrols"])
     env.context_class = _LazyContext
     env.filters.update(FILTERS)

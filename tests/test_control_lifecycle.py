@@ -199,3 +199,67 @@ def test_app_deploy_nginx_and_training_chart(control):
     for bad in ({"release": "x; rm -rf /"}, {"chart": "../etc"}, {"namespace": "A B"}, {"values": [1]}):
         with pytest.raises(ValueError):
             deploy.create("demo", "app-deploy", bad, run="none")
+
+
+def test_bigip_config_attaches_virtual_servers(control):
+    """F5 BIG-IP (reference roles/f5/tasks/main.yml:1-39): controller with RBAC, readiness poll, then a virtual
+    server on every add-on ingress (HTTP annotations; HTTPS: client-SSL TLS patch + server-SSL annotation), and
+    the ingresses report the BIG-IP address."""
+    _cluster()
+    assert deploy.create("demo", "install", run="inline")["state"] == "SUCCESS"
+    clusters.set_config("demo", "bigip_url", "https://10.9.9.9")
+    clusters.set_config("demo", "public_ip", "10.9.9.100")
+    e = deploy.create("demo", "bigip-config", run="inline")
+    assert e["state"] == "SUCCESS", e["result_summary"].get("dark")
+    log = [c for _, c in control.farm.log]
+    ann = [c for c in log if "annotate ingress" in c]
+    for name in ("f2c-grafana", "registry-ui", "weave-scope", "kubeapps-plus", "dashboard-kubernetes-dashboard"):
+        assert any(f" {name} " in c and "virtual-server.f5.com/ip=10.9.9.100" in c for c in ann), name
+    assert any("serverssl=/Common/serverssl" in c and "dashboard" in c for c in ann)
+    assert any("patch ingress dashboard-kubernetes-dashboard" in c and "/Common/clientssl" in c for c in log)
+    assert any("get deploy k8s-bigip-ctlr" in c for c in log)
+    ctlr = control.farm.fs["m1"]["/opt/kubeoperator/manifests/bigip-ctlr.yaml"].decode()
+    assert "serviceAccountName: bigip-ctlr" in ctlr and "--bigip-url=https://10.9.9.9" in ctlr
+    # without the endpoint the operation refuses (cluster state unchanged: bigip errors are ignored)
+    clusters.set_config("demo", "bigip_url", "")
+    assert deploy.create("demo", "bigip-config", run="inline")["state"] == "FAILURE"
+    assert clusters.get_cluster("demo").status == "RUNNING"
+
+
+def test_addons_include_weave_scope_and_the_kubeapps_store(control):
+    _cluster()
+    assert deploy.create("demo", "install", run="inline")["state"] == "SUCCESS"
+    log = [c for _, c in control.farm.log]
+    assert any("kubectl apply -f /opt/kubeoperator/manifests/weave-scope.yaml" in c for c in log)
+    assert any("helm upgrade --install kubeapps-plus kubeoperator/kubeapps" in c for c in log)
+    vals = control.farm.fs["m1"]["/opt/kubeoperator/manifests/kubeapps-values.yaml"].decode()
+    assert "chartmuseum.kube-operator.svc.cluster.local:8080" in vals and "apps." in vals
+    uploads = [c for c in log if "api/charts?force" in c]
+    assert {u.split("helm package ")[1].split()[0] for u in uploads} >= {"pytorch-rocm-train", "pytorch-rocm-serve"}
+
+
+def test_os_hardening_is_opt_in_and_kubernetes_safe(control):
+    """OS hardening (reference roles/os-harden, dormant there): off by default; with os_hardening_enabled the
+    prepare step writes the sysctl / login / pam / limits / modprobe / audit policy on every node, keeps the
+    forwarding and bridge settings Kubernetes needs (checked), and the install still succeeds."""
+    _cluster()
+    assert deploy.create("demo", "install", run="inline")["state"] == "SUCCESS"
+    assert not any("90-kubeoperator-hardening" in p for fs in control.farm.fs.values() for p in fs)
+    clusters.set_config("demo", "os_hardening_enabled", True)
+    e = deploy.create("demo", "install", run="inline")
+    assert e["state"] == "SUCCESS", e["result_summary"].get("dark")
+    for h in ("m1", "w1"):
+        fs = control.farm.fs[h]
+        sysctl = fs["/etc/sysctl.d/90-kubeoperator-hardening.conf"].decode()
+        assert "kernel.kptr_restrict = 2" in sysctl and "ip_forward" not in sysctl
+        mp = fs["/etc/modprobe.d/kubeoperator-hardening.conf"].decode()
+        assert "install cramfs /bin/true" in mp and "amdgpu" not in mp and "squashfs" not in mp
+        assert b"-w /etc/kubernetes/ -p wa -k kubernetes" in fs["/etc/audit/rules.d/kubeoperator.rules"]
+        assert b"* hard core 0" in fs["/etc/security/limits.d/10-kubeoperator-hardening.conf"]
+    cmds = control.farm.commands("w1")
+    assert "sysctl -n net.ipv4.ip_forward net.bridge.bridge-nf-call-iptables" in cmds
+    assert any(c.startswith("usermod -s /usr/sbin/nologin daemon") for c in cmds)
+    assert not any("usermod -s /usr/sbin/nologin root" in c for c in cmds)
+    # a node whose forwarding the hardening would break fails the step instead of continuing
+    control.farm.add_rule(r"^sysctl -n net\.ipv4\.ip_forward", stdout="0\n1")
+    assert deploy.create("demo", "install", run="inline")["state"] == "FAILURE"

@@ -217,8 +217,9 @@ def load_model(name: str, device: str, ckpt: str = ""):
     return m
 
 
-def main(argv=None) -> int:
-    ap = argparse.ArgumentParser()
+def build_parser() -> argparse.ArgumentParser:
+    """The server's arguments (also what the serving chart's rendered args are checked against)."""
+    ap = argparse.ArgumentParser(prog="kubeoperator_amd.serve.server")
     ap.add_argument("--model", default="llama3_8b")
     ap.add_argument("--max-batch", type=int, default=64)
     ap.add_argument("--max-seq", type=int, default=8192)
@@ -227,7 +228,11 @@ def main(argv=None) -> int:
     ap.add_argument("--ckpt", default="")
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=8000)
-    a = ap.parse_args(argv)
+    return ap
+
+
+def main(argv=None) -> int:
+    a = build_parser().parse_args(argv)
     import uvicorn
 
     dev = "cuda" if torch.cuda.is_available() else "cpu"

@@ -14,8 +14,9 @@ import sys
 import time
 
 
-def main(argv=None) -> int:
-    ap = argparse.ArgumentParser()
+def build_parser() -> argparse.ArgumentParser:
+    """The CLI's arguments (also what the training chart's rendered Job args are checked against)."""
+    ap = argparse.ArgumentParser(prog="kubeoperator_amd.train.cli")
     ap.add_argument("--model", default="llama3_8b")
     ap.add_argument("--seq", type=int, default=8192)
     ap.add_argument("--mbs", type=int, default=1)
@@ -40,10 +41,9 @@ def main(argv=None) -> int:
     ap.add_argument("--recompute", type=int, default=0, choices=[0, 1],
                     help="per-block activation recompute: only block inputs stay saved (long sequences, e.g. "
                          "Llama-3-8B at --seq 32768 on one GPU; ~1/3 more FLOPs)")
-    ap.add_argument("--wgrad-stream", default="off", choices=["auto", "on", "off"],
-                    help="weight-gradient GEMMs on a second HIP stream beside the data-gradient chain, one rank only "
-                         "(auto: models narrower than 2048, +8 %% on GPT-2-small). Off by default: the one-GPU "
-                         "multi-process rehearsal showed sporadic divergence with it (profiles/r2_experiments.md)")
+    ap.add_argument("--wgrad-stream", default="auto", choices=["auto", "on", "off"],
+                    help="weight-gradient GEMMs on a second HIP stream beside the data-gradient chain (auto: models "
+                         "narrower than 2048, +8 %% on GPT-2-small)")
     ap.add_argument("--grad-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="gradient buffer precision (fp32: accumulation and DP reduction in fp32)")
     ap.add_argument("--cuda-graph", type=int, default=0, choices=[0, 1],
@@ -57,7 +57,11 @@ def main(argv=None) -> int:
                     help="fault injection 'RANK:STEP': that rank dies abruptly after finishing STEP (before its "
                          "checkpoint) on the first attempt only (TORCHELASTIC_RESTART_COUNT 0), to exercise "
                          "torchrun --max-restarts + --resume")
-    a = ap.parse_args(argv)
+    return ap
+
+
+def main(argv=None) -> int:
+    a = build_parser().parse_args(argv)
     fault = None
     if a.inject_fault:
         fr, _, fs = a.inject_fault.partition(":")

@@ -87,7 +87,7 @@ def main() -> int:
                          "Llama-3-8B at --seq 32768 on one GPU; ~1/3 more FLOPs)")
     ap.add_argument("--wgrad-stream", default="auto", choices=["auto", "on", "off"],
                     help="weight-gradient GEMMs on a second HIP stream beside the data-gradient chain (auto: models "
-                         "narrower than 2048, +8 %% on GPT-2-small; single-rank jobs unless KOP_WGRAD_STREAM_MULTI=1)")
+                         "narrower than 2048, +8 %% on GPT-2-small)")
     ap.add_argument("--grad-dtype", default="bf16", choices=["bf16", "fp32"],
                     help="gradient buffer precision (fp32: accumulation and DP reduction in fp32)")
     ap.add_argument("--cuda-graph", type=int, default=0, choices=[0, 1],

@@ -188,7 +188,8 @@ views["cluster-create"] = async (v) => {
       const need = r.meta?.requires?.nodes_require;
       if (!Array.isArray(need) || r.meta?.hidden) continue;
       const n = counts[r.name] || 0, [op, k] = need;
-      const ok = op === "=" ? n === k : op === ">=" ? n >= k : op === ">" ? n > k : true;
+      // ">" means "at least k" as in the reference wizard (cluster-create.component.ts:307-312 opens k node slots)
+      const ok = op === "=" ? n === k : (op === ">=" || op === ">") ? n >= k : true;
       if (!ok) msgs.push(`role ${r.name}: needs ${op} ${k} node(s), selected ${n}`);
     }
     $("#checks").innerHTML = msgs.length ? `<p class="error">${msgs.map(esc).join("<br>")}</p>` : "";
@@ -347,7 +348,8 @@ views.cluster = async (v, [name, tab = "overview", arg]) => {
         ["Class", (x) => esc(x.spec.storageClassName)], ["Size", (x) => esc(((x.spec.resources || {}).requests || {}).storage)], ["Phase", (x) => st((x.status || {}).phase)]])}`;
   } else if (tab === "f5") {
     const cfgs = Object.fromEntries((await GET(`/clusters/${name}/configs/`)).map((x) => [x.key, x.value]));
-    const keys = [["bigip_host", "BIG-IP address"], ["bigip_port", "Port"], ["bigip_user", "User"], ["bigip_password", "Password"], ["bigip_partition", "Partition"], ["bigip_public_ip", "Virtual server IP"]];
+    // the variables of roles/f5 (k8s-bigip-ctlr --bigip-url, credentials secret, virtual-server address)
+    const keys = [["bigip_url", "BIG-IP URL (https://host[:port])"], ["bigip_user", "User"], ["bigip_password", "Password"], ["bigip_partition", "Partition"], ["public_ip", "Virtual server IP"]];
     t.innerHTML = `<form id="f5" class="card">${keys.map(([k, l]) => `<label>${esc(l)}<input name="${k}" type="${k.includes("password") ? "password" : "text"}" value="${esc(k.includes("password") ? "" : (cfgs[k] ?? ""))}"></label>`).join("")}
       <div class="toolbar"><button type="submit">Save &amp; configure F5</button></div><p class="error" id="f5-err"></p></form>`;
     $("#f5").addEventListener("submit", async (e) => {

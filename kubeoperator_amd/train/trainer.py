@@ -104,12 +104,8 @@ class Trainer:
         env = os.environ.get("KOP_WGRAD_STREAM")
         want = (tc.wgrad_stream == "on" or (tc.wgrad_stream == "auto" and self.cfg.hidden < 2048)) \
             if env not in ("0", "1") else env == "1"
-        # multi-rank jobs (data or tensor parallel) only with KOP_WGRAD_STREAM_MULTI=1 until the one-GPU
-        # multi-rank rehearsal confirms the in-place-accumulation fix (ops.functional._sink) there as well
-        if want and info.world > 1 and os.environ.get("KOP_WGRAD_STREAM_MULTI") != "1":
-            if tc.wgrad_stream == "on" or env == "1":
-                raise ValueError("the weight-gradient side stream is single-rank only (wgrad_stream on, world > 1)")
-            want = False
+        # multi-rank jobs included: the 2-4 rank data- / tensor-parallel rehearsals on one MI355X with the side stream
+        # forced to lag match one process to bf16 reduction noise (profiles/r3_wgrad_multirank_rehearsal.jsonl)
         self.store.wgrad_stream = dev.type == "cuda" and not tc.cuda_graph and want
         self.opt = FusedAdamW(self.dp.optimizer_segments(), lr=tc.lr, betas=tc.betas, eps=tc.eps,
                               weight_decay=tc.weight_decay, max_grad_norm=tc.grad_clip,

@@ -18,6 +18,14 @@ def _env():
     return env
 
 
+def _port() -> str:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return str(s.getsockname()[1])
+
+
 def _json_lines(out: str):
     return [json.loads(line) for line in out.splitlines() if line.startswith("{")]
 
@@ -46,14 +54,14 @@ def test_bench_self_launches_ranks_without_torchrun():
 
 def test_bench_under_torchrun_unchanged():
     lines = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
-                  "--master-addr", "127.0.0.1", "--master-port", "29731", "bench.py", "--gpus", "2"] + ARGS)
+                  "--master-addr", "127.0.0.1", "--master-port", _port(), "bench.py", "--gpus", "2"] + ARGS)
     assert len(lines) == 1 and lines[0]["n_gpus"] == 2 and lines[0]["rccl_world"] == 2
 
 
 def test_bench_refuses_mismatched_world():
     env = _env()
     p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", "29733", "bench.py", "--gpus", "4"] + ARGS,
+                        "--master-addr", "127.0.0.1", "--master-port", _port(), "bench.py", "--gpus", "4"] + ARGS,
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode != 0
     assert not _json_lines(p.stdout)

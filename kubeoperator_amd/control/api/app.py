@@ -1023,6 +1023,66 @@ def create_app() -> FastAPI:
         except Exception as e:  # noqa: BLE001
             return {"success": False, "detail": str(e)}
 
+    # ------------------------------------------------------------------ task monitor (the reference's Flower)
+    @r.get("/tasks/")
+    def task_list(request: Request):
+        """Recent jobs, newest first; filters state / name, limit (default 100, at most 1000)."""
+        superuser(request)
+        q = request.query_params
+        limit = min(1000, int(q.get("limit", 100) or 100))
+        with session_scope() as s:
+            stmt = select(M.Job).order_by(M.Job.date_created.desc()).limit(limit)
+            if q.get("state"):
+                stmt = stmt.where(M.Job.state == q["state"].upper())
+            if q.get("name"):
+                stmt = stmt.where(M.Job.name == q["name"])
+            rows = list(s.scalars(stmt))
+            return [{"id": j.id, "name": j.name, "state": j.state, "worker": j.worker, "attempts": j.attempts,
+                     "args": j.args, "date_created": j.date_created, "date_start": j.date_start, "date_end": j.date_end,
+                     "runtime_s": (j.date_end - j.date_start).total_seconds() if j.date_end and j.date_start else None,
+                     "error": (j.result or {}).get("error")} for j in rows]
+
+    @r.get("/tasks/stats/")
+    def task_stats(request: Request):
+        superuser(request)
+        hours = request.query_params.get("hours")
+        since = M.now() - dt.timedelta(hours=float(hours)) if hours else None
+        return {"tasks": jobs.stats(since), "registered": jobs.registered_tasks()}
+
+    @r.get("/tasks/workers/")
+    def task_workers(request: Request):
+        superuser(request)
+        return jobs.workers()
+
+    @r.get("/tasks/periodic/")
+    def task_periodic(request: Request):
+        superuser(request)
+        with session_scope() as s:
+            return [{"name": p.name, "task": p.task, "crontab": p.crontab, "interval_s": p.interval_s,
+                     "enabled": p.enabled, "last_run": p.last_run}
+                    for p in s.scalars(select(M.PeriodicTask).order_by(M.PeriodicTask.name))]
+
+    @r.post("/tasks/{jid}/revoke/")
+    def task_revoke(jid: str, request: Request):
+        superuser(request)
+        try:
+            changed, state = jobs.revoke(jid)
+        except KeyError:
+            raise HTTPError(404, f"task {jid} not found")
+        if not changed:
+            raise HTTPError(409, f"task {jid} is {state}: only a PENDING task can be revoked")
+        return {"id": jid, "state": state}
+
+    @r.post("/tasks/{jid}/retry/")
+    def task_retry(jid: str, request: Request):
+        superuser(request)
+        try:
+            return {"id": jobs.retry(jid), "retry_of": jid}
+        except KeyError:
+            raise HTTPError(404, f"task {jid} not found")
+        except ValueError as e:
+            raise HTTPError(409, str(e))
+
     # ------------------------------------------------------------------ tasks (celery_api/api.py:15-37)
     @r.get("/tasks/{jid}/result/")
     def task_result(jid: str, request: Request):
@@ -1039,7 +1099,7 @@ def create_app() -> FastAPI:
         off = int(request.query_params.get("mark", request.query_params.get("offset", 0)) or 0)
         data, end = jobs.tail(jobs.log_path(jid), off, 1 << 20)
         j = jobs.get(jid)
-        return {"data": data, "mark": end, "end": j is not None and j.state in ("SUCCESS", "FAILURE")}
+        return {"data": data, "mark": end, "end": j is not None and j.state in ("SUCCESS", "FAILURE", "REVOKED")}
 
     # ------------------------------------------------------------------ training chart (bundled workload)
     @r.get("/train/presets/")
@@ -1095,7 +1155,7 @@ def create_app() -> FastAPI:
                     off = off2
                     continue
                 j = await asyncio.to_thread(jobs.get, jid)
-                if j is not None and j.state in ("SUCCESS", "FAILURE"):
+                if j is not None and j.state in ("SUCCESS", "FAILURE", "REVOKED"):
                     idle_after_end += 1
                     if idle_after_end > 2:
                         break
@@ -1108,6 +1168,12 @@ def create_app() -> FastAPI:
     @app.get("/")
     def root():
         return RedirectResponse("/ui/")
+
+    @app.get("/flower/")
+    def flower():
+        """The reference proxies Celery Flower here (kubeoperator/celery_flower.py:13-22): its task monitor is
+        the UI's tasks view."""
+        return RedirectResponse("/ui/#/tasks")
 
     @app.get("/ui/{path:path}")
     def ui(path: str):

@@ -9,6 +9,10 @@ convention (celery_api/utils.py:212-217) -- which the log API / websocket tail.
 Recovery: at worker start every job left STARTED by a dead worker is marked FAILURE (and its
 execution too), instead of the reference's "mark the previous STARTED execution FAILURE when a new one
 starts" (kubeops_api/api.py:244-248).
+
+Task monitor (the reference runs Celery Flower, core/kubeops.py:197-213, proxied at /flower/): every worker
+process keeps a heartbeat row (jobs running, jobs processed, last seen); ``stats`` aggregates the job table per
+task name; a PENDING job can be revoked (REVOKED: never claimed) and a finished one retried as a new job.
 """
 from __future__ import annotations
 
@@ -100,6 +104,63 @@ def get(job_id: str) -> M.Job | None:
         return s.get(M.Job, job_id)
 
 
+def revoke(job_id: str) -> tuple[bool, str]:
+    """PENDING -> REVOKED (a worker never claims it): (True, "REVOKED"). Any other state -- a running job cannot
+    be stopped from outside its thread -- is left alone: (False, state)."""
+    with session_scope() as s:
+        n = s.execute(update(M.Job).where(M.Job.id == job_id, M.Job.state == "PENDING")
+                      .values(state="REVOKED", date_end=M.now(), result={"error": "revoked"})).rowcount
+        j = s.get(M.Job, job_id)
+        if j is None:
+            raise KeyError(job_id)
+        return (True, "REVOKED") if n else (False, j.state)
+
+
+def retry(job_id: str) -> str:
+    """Submit a finished (FAILURE / REVOKED / SUCCESS) job again with the same task and arguments."""
+    j = get(job_id)
+    if j is None:
+        raise KeyError(job_id)
+    if j.state in ("PENDING", "STARTED"):
+        raise ValueError(f"job {job_id} is {j.state}")
+    return submit(j.name, dict(j.args or {}))
+
+
+def stats(since: "dt.datetime | None" = None) -> list[dict]:
+    """Per task name: job counts by state and run-time statistics of the finished ones."""
+    import collections
+
+    agg: dict = collections.defaultdict(lambda: {"states": collections.Counter(), "runtimes": []})
+    with session_scope() as s:
+        q = select(M.Job.name, M.Job.state, M.Job.date_start, M.Job.date_end)
+        if since is not None:
+            q = q.where(M.Job.date_created >= since)
+        for name, state, t0, t1 in s.execute(q):
+            a = agg[name]
+            a["states"][state] += 1
+            if t0 is not None and t1 is not None:
+                a["runtimes"].append((t1 - t0).total_seconds())
+    out = []
+    for name, a in sorted(agg.items()):
+        rt = sorted(a["runtimes"])
+        out.append({"task": name, "total": sum(a["states"].values()), **{k.lower(): v for k, v in a["states"].items()},
+                    "runtime_avg_s": round(sum(rt) / len(rt), 3) if rt else None,
+                    "runtime_p50_s": round(rt[len(rt) // 2], 3) if rt else None,
+                    "runtime_max_s": round(rt[-1], 3) if rt else None})
+    return out
+
+
+def workers(online_after_s: float = 30.0) -> list[dict]:
+    now = M.now()
+    with session_scope() as s:
+        rows = list(s.scalars(select(M.WorkerHeartbeat).order_by(M.WorkerHeartbeat.name)))
+        return [{"name": w.name, "hostname": w.hostname, "pid": w.pid, "concurrency": w.concurrency,
+                 "started": w.started, "last_seen": w.last_seen, "active": list(w.active or []),
+                 "processed": w.processed,
+                 "online": (not w.stopped and w.last_seen is not None
+                            and (now - w.last_seen).total_seconds() < online_after_s)} for w in rows]
+
+
 def _claim(worker: str) -> M.Job | None:
     with session_scope() as s:
         for j in s.scalars(select(M.Job).where(M.Job.state == "PENDING").order_by(M.Job.date_created).limit(8)):
@@ -160,25 +221,50 @@ _wake = threading.Event()
 
 
 class WorkerPool:
-    def __init__(self, concurrency: int | None = None, poll_s: float = 1.0):
+    def __init__(self, concurrency: int | None = None, poll_s: float = 1.0, heartbeat_s: float = 5.0):
         from ..conf import get_config
 
         self.concurrency = concurrency or int(get_config()["WORKER_CONCURRENCY"])
         self.poll_s = poll_s
-        self.name = f"{socket.gethostname()}:{os.getpid()}"
+        self.heartbeat_s = heartbeat_s
+        self.name = f"{socket.gethostname()}:{os.getpid()}:{id(self) & 0xffff:04x}"
         self._stop = threading.Event()
         self._threads: list[threading.Thread] = []
+        self._active: set = set()
+        self._processed = 0
+        self._lock = threading.Lock()
 
     def start(self, recover: bool = True):
         if recover:
             n = recover_orphans()
             if n:
                 log.warning("recovered %d orphaned jobs", n)
+        with session_scope() as s:
+            s.merge(M.WorkerHeartbeat(name=self.name, hostname=socket.gethostname(), pid=os.getpid(),
+                                      concurrency=self.concurrency, started=M.now(), last_seen=M.now(), active=[],
+                                      processed=0, stopped=False))
         for i in range(self.concurrency):
             t = threading.Thread(target=self._loop, name=f"kop-worker-{i}", daemon=True)
             t.start()
             self._threads.append(t)
+        hb = threading.Thread(target=self._heartbeat_loop, name="kop-worker-heartbeat", daemon=True)
+        hb.start()
+        self._threads.append(hb)
         return self
+
+    def _beat(self, stopped: bool = False) -> None:
+        with self._lock:
+            active, processed = sorted(self._active), self._processed
+        with session_scope() as s:
+            s.execute(update(M.WorkerHeartbeat).where(M.WorkerHeartbeat.name == self.name)
+                      .values(last_seen=M.now(), active=active, processed=processed, stopped=stopped))
+
+    def _heartbeat_loop(self):
+        while not self._stop.wait(self.heartbeat_s):
+            try:
+                self._beat()
+            except Exception:  # noqa: BLE001 - a missed heartbeat is not fatal
+                log.exception("worker heartbeat failed")
 
     def _loop(self):
         while not self._stop.is_set():
@@ -187,10 +273,23 @@ class WorkerPool:
                 _wake.wait(self.poll_s)
                 _wake.clear()
                 continue
-            run_job(job)
+            with self._lock:
+                self._active.add(job.id)
+            self._beat()
+            try:
+                run_job(job)
+            finally:
+                with self._lock:
+                    self._active.discard(job.id)
+                    self._processed += 1
+                self._beat()
 
     def stop(self, timeout: float = 5.0):
         self._stop.set()
         _wake.set()
         for t in self._threads:
             t.join(timeout)
+        try:
+            self._beat(stopped=True)
+        except Exception:  # noqa: BLE001
+            pass

@@ -383,6 +383,21 @@ class Job(IdMixin, Base):
     attempts: Mapped[int] = mapped_column(Integer, default=0)
 
 
+class WorkerHeartbeat(Base):
+    """One row per job-worker process (the task monitor's worker list; reference Celery Flower workers view,
+    core/kubeops.py:197-213)."""
+    __tablename__ = "worker_heartbeats"
+    name: Mapped[str] = mapped_column(String(128), primary_key=True)  # host:pid
+    hostname: Mapped[str] = mapped_column(String(128), default="")
+    pid: Mapped[int] = mapped_column(Integer, default=0)
+    concurrency: Mapped[int] = mapped_column(Integer, default=1)
+    started: Mapped[_dt.datetime | None] = mapped_column(DateTime, nullable=True)
+    last_seen: Mapped[_dt.datetime | None] = mapped_column(DateTime, nullable=True)
+    active: Mapped[list] = mapped_column(JSON, default=list)  # job ids running now
+    processed: Mapped[int] = mapped_column(Integer, default=0)
+    stopped: Mapped[bool] = mapped_column(Boolean, default=False)
+
+
 class PeriodicTask(IdMixin, Base):
     """Cron-like schedule entry (reference django-celery-beat rows; celery_api/utils.py:59-181)."""
     __tablename__ = "periodic_tasks"

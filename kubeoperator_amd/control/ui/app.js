@@ -545,13 +545,41 @@ views.training = async (v) => {
     <h3>Model presets</h3>${table(Object.entries(presets).map(([k, p]) => ({name: k, ...p})), [["Preset", "name"], ["Parameters", (p) => `${(p.params / 1e9).toFixed(2)} B`], ["Layers", "layers"], ["Hidden", "hidden"]])}`;
 };
 
+// task monitor (the reference's Celery Flower at /flower/): workers, per-task statistics, recent jobs with
+// revoke / retry and their logs, the periodic schedule
+views.tasks = async (v, [state = ""]) => {
+  const [workers, stats, recent, periodic] = await Promise.all([GET("/tasks/workers/"), GET("/tasks/stats/"),
+    GET(`/tasks/?limit=200${state ? "&state=" + encodeURIComponent(state) : ""}`), GET("/tasks/periodic/")]);
+  const secs = (x) => (x === null || x === undefined ? "" : `${Number(x).toFixed(2)} s`);
+  v.innerHTML = `<h2>Task monitor</h2>
+    <h3>Workers</h3>${table(workers, [["Worker", "name"], ["Online", (w) => st(w.online ? "online" : "offline")], ["Concurrency", "concurrency"],
+      ["Running", (w) => (w.active || []).length], ["Processed", "processed"], ["Last seen", "last_seen"]], "No worker process has registered.")}
+    <h3>Tasks</h3>${table(stats.tasks, [["Task", "task"], ["Total", "total"], ["Succeeded", (t) => t.success || 0], ["Failed", (t) => t.failure || 0],
+      ["Pending", (t) => t.pending || 0], ["Running", (t) => t.started || 0], ["Avg", (t) => secs(t.runtime_avg_s)], ["Max", (t) => secs(t.runtime_max_s)]])}
+    <h3>Recent jobs</h3><div class="toolbar">${["", "PENDING", "STARTED", "SUCCESS", "FAILURE", "REVOKED"].map((s) =>
+      `<a href="#/tasks/${s}" class="${s === state ? "active" : ""}">${s || "all"}</a>`).join(" ")}</div>
+    ${table(recent, [["Task", "name"], ["State", (j) => st(j.state)], ["Worker", "worker"], ["Created", "date_created"], ["Runtime", (j) => secs(j.runtime_s)],
+      ["Error", "error"], ["", (j) => `<button class="link" data-log="${esc(j.id)}">log</button>` +
+        (j.state === "PENDING" ? `<button class="link" data-revoke="${esc(j.id)}">revoke</button>` : "") +
+        (["FAILURE", "REVOKED"].includes(j.state) ? `<button class="link" data-retry="${esc(j.id)}">retry</button>` : "")]], "No jobs.")}
+    <h3>Periodic schedule</h3>${table(periodic, [["Name", "name"], ["Task", "task"], ["Cron", "crontab"], ["Every", (p) => p.interval_s ? `${p.interval_s} s` : ""],
+      ["Enabled", "enabled"], ["Last run", "last_run"]])}
+    <pre class="term hidden" id="joblog"></pre>`;
+  v.querySelectorAll("[data-revoke]").forEach((b) => b.onclick = () => confirmDo("Revoke this job?", () => POST(`/tasks/${b.dataset.revoke}/revoke/`)));
+  v.querySelectorAll("[data-retry]").forEach((b) => b.onclick = () => confirmDo("Run this job again?", () => POST(`/tasks/${b.dataset.retry}/retry/`)));
+  v.querySelectorAll("[data-log]").forEach((b) => b.onclick = async () => {
+    const r = await GET(`/tasks/${b.dataset.log}/log/`);
+    const pre = $("#joblog"); pre.classList.remove("hidden"); pre.textContent = r.data;
+  });
+};
+
 // ------------------------------------------------------------------ navigation
 const NAV = [["Overview", [["dashboard", "Dashboard"], ["clusters", "Clusters"], ["training", "GPU training"]]],
   ["Infrastructure", [["hosts", "Hosts"], ["credentials", "Credentials"], ["regions", "Regions"], ["zones", "Zones"], ["plans", "Deploy plans"], ["packages", "Packages"], ["storage", "Storage"]]],
-  ["Administration", [["items", "Items"], ["users", "Users"], ["settings", "Settings"], ["messages", "Messages"], ["logs", "System log"], ["profile", "Profile"]]]];
+  ["Administration", [["items", "Items"], ["users", "Users"], ["settings", "Settings"], ["tasks", "Task monitor"], ["messages", "Messages"], ["logs", "System log"], ["profile", "Profile"]]]];
 
 function renderNav(current) {
-  $("#nav").innerHTML = NAV.map(([g, items]) => `<div class="group">${g}</div>` + items.filter(([k]) => ME.is_superuser || !["users", "settings", "credentials"].includes(k))
+  $("#nav").innerHTML = NAV.map(([g, items]) => `<div class="group">${g}</div>` + items.filter(([k]) => ME.is_superuser || !["users", "settings", "credentials", "tasks"].includes(k))
     .map(([k, label]) => `<a href="#/${k}" class="${k === current ? "active" : ""}">${label}</a>`).join("")).join("");
 }
 

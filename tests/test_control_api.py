@@ -238,3 +238,60 @@ def test_app_catalog_and_deploy_over_http(client):
     assert e["state"] == "SUCCESS" and e["result_summary"]["training"]["tokens_per_s"] > 0
     apps = client.get("/api/v1/clusters/demo/apps/").json()
     assert [a["release"] for a in apps] == ["gpt2"] and apps[0]["values"]["model"] == "gpt2_small"
+
+
+def test_task_monitor_workers_stats_revoke_retry(client):
+    """The Flower equivalent (reference core/kubeops.py:197-213, /flower/ proxy): worker heartbeats, per-task
+    statistics, recent jobs, revoke of a queued job, retry of a failed one."""
+    from kubeoperator_amd.control.runtime import jobs
+
+    calls = []
+
+    @jobs.task("monitor_probe")
+    def probe(job_id, logger, fail=False):
+        calls.append(job_id)
+        logger.info("probe ran")
+        if fail:
+            raise RuntimeError("probe failed on purpose")
+        return {"ok": True}
+
+    queued = jobs.submit("monitor_probe", {})
+    r = client.post(f"/api/v1/tasks/{queued}/revoke/")
+    assert r.status_code == 200 and r.json()["state"] == "REVOKED"
+    assert client.post(f"/api/v1/tasks/{queued}/revoke/").status_code == 409  # not PENDING any more
+    ok = jobs.submit("monitor_probe", {})
+    bad = jobs.submit("monitor_probe", {"fail": True})
+    pool = jobs.WorkerPool(concurrency=2, poll_s=0.02, heartbeat_s=0.05).start()
+    try:
+        for _ in range(200):
+            if jobs.get(ok).state == "SUCCESS" and jobs.get(bad).state == "FAILURE":
+                break
+            time.sleep(0.02)
+        for _ in range(200):  # the heartbeat follows the job's end
+            w = client.get("/api/v1/tasks/workers/").json()
+            if any(x["online"] and x["name"] == pool.name and x["processed"] >= 2 for x in w):
+                break
+            time.sleep(0.02)
+        assert any(x["online"] and x["name"] == pool.name and x["processed"] >= 2 for x in w), w
+        assert queued not in calls  # revoked: never ran
+        st = {t["task"]: t for t in client.get("/api/v1/tasks/stats/").json()["tasks"]}
+        p = st["monitor_probe"]
+        assert p["total"] == 3 and p["success"] == 1 and p["failure"] == 1 and p["revoked"] == 1
+        assert p["runtime_avg_s"] is not None
+        fails = client.get("/api/v1/tasks/?state=failure&name=monitor_probe").json()
+        assert [j["id"] for j in fails] == [bad] and "on purpose" in fails[0]["error"]
+        r = client.post(f"/api/v1/tasks/{bad}/retry/")
+        assert r.status_code == 200 and r.json()["retry_of"] == bad
+        again = r.json()["id"]
+        for _ in range(200):
+            if jobs.get(again).state in ("SUCCESS", "FAILURE"):
+                break
+            time.sleep(0.02)
+        assert jobs.get(again).state == "FAILURE" and jobs.get(again).args == {"fail": True}
+        assert "probe ran" in client.get(f"/api/v1/tasks/{again}/log/").json()["data"]
+    finally:
+        pool.stop()
+    w = client.get("/api/v1/tasks/workers/").json()
+    assert not next(x for x in w if x["name"] == pool.name)["online"]  # stopped
+    assert client.get("/flower/", follow_redirects=False).headers["location"] == "/ui/#/tasks"
+    assert isinstance(client.get("/api/v1/tasks/periodic/").json(), list)

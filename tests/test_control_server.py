@@ -169,7 +169,7 @@ def test_ui_script_parses_and_covers_the_reference_modules():
     src = open(path).read()
     views = set(re.findall(r"^views(?:\.|\[\")([\w-]+)", src, re.M))
     assert {"dashboard", "clusters", "cluster-create", "cluster", "hosts", "credentials", "packages", "regions", "zones",
-            "plans", "storage", "items", "users", "settings", "messages", "logs", "profile", "training"} <= views, views
+            "plans", "storage", "items", "users", "settings", "messages", "logs", "profile", "training", "tasks"} <= views, views
     for tab in ("overview", "nodes", "deploy", "apps", "health", "events", "storage", "backup", "grade", "configs",
                 "f5", "terminal"):
         assert f'tab === "{tab}"' in src or tab == "overview", tab

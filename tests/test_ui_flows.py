@@ -62,3 +62,4 @@ def test_ui_flows_against_a_live_control_plane(control):
     assert all(s[1] == "success" for s in inst["steps"][:5]) and not inst["socket_errors"]
     assert inst["log_bytes"] > 1000
     assert "llama-train" in by["app-deployed"]["row"] and "tokens/s" in by["app-deployed"]["row"]
+    assert by["task-monitor"]["recent_jobs"] >= 2  # the install and the app deploy

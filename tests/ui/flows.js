@@ -193,6 +193,14 @@ async function main() {
   const row = await until(() => doc.querySelectorAll("#tab table tr").find((r) => /llama-train/.test(r.textContent)), "release row");
   if (!/tokens\/s/.test(row.textContent)) throw new Error("no training result in the release row: " + row.textContent);
   log("app-deployed", {row: row.textContent.replace(/\s+/g, " ").trim()});
+  // ------------------------------------------------------------------ task monitor (the reference's Flower)
+  win.location.hash = "#/tasks";
+  await until(() => /Task monitor/.test($("#view").textContent) && /online/.test($("#view").textContent), "task monitor with an online worker");
+  const kids = $("#view").children;
+  const h = kids.findIndex((el) => el.localName === "h3" && el.textContent === "Recent jobs");
+  const jobTable = kids.slice(h + 1).find((el) => el.localName === "table");
+  const jobRows = jobTable.querySelectorAll("tr").length - 1;
+  log("task-monitor", {recent_jobs: jobRows});
   if (alerts.length) throw new Error("unexpected alerts: " + alerts.join("; "));
   sockets.forEach((s) => s.close());
   log("done");

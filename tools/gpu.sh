@@ -1,0 +1,163 @@
+#!/bin/bash
+# GPU sessions on a one-GPU MI355X box, one entry point:
+#   /usr/local/graft/bin/gpurun --timeout N -- bash tools/gpu.sh <session> [<session> ...]
+# Sessions run in order and stop at the first failing step (every step has its own time limit, no retries).
+# Logs land in gpurun_out/<step>.log; the summaries worth keeping are copied into profiles/.
+#
+#   check        GPU test suite, smoke(), Llama-3-8B and GPT-2-small benches (what the driver runs at round end)
+#   tests        the GPU test suite only (SEL=<pytest selection> narrows it)
+#   bench        Llama-3-8B bench (ARGSETS="--a;--b" runs several argument sets back to back: same-box A/B)
+#   gpt2         GPT-2-small bench (ARGSETS as above)
+#   prof-l8b     rocprofv3 kernel trace + stats of the Llama-3-8B step
+#   prof-gpt2    rocprofv3 kernel trace + stats of the GPT-2-small step
+#   pmc-attn     PMC counter passes (one rocprofv3 run each) over the attention micro-benchmark
+#   attn-probe   attention TF/s per shape; VARIANTS="ENV=a;ENV=b;base" alternates env variants twice
+#   dp           one-GPU data-parallel rehearsals (2 / 4 gloo ranks sharing cuda:0) + bench.py --gpus 2 under torchrun
+#   tp           one-GPU tensor (+ sequence) parallel rehearsals + bench.py --tp 2 [--sp 1] + 4 Llama-3-70B layers
+#   wgrad-lag    weight-gradient side stream under a forced lag: GPU tests, then DP / TP rehearsals with it on
+#   wgrad-splitk weight-gradient GEMM forms at the training shapes (tools/bench_wgrad_splitk.py)
+#   tune         TunableOp tuning of the training GEMMs, then heuristic vs tuned bench
+#   tune-decode  TunableOp tuning of the decode GEMMs, then the decode benchmark
+#   serve        serving tests, decode benchmark, continuous-batching benchmark
+#   fp8          FP8 GPU tests and the opt-in --fp8 Llama-3-8B bench
+source "$(dirname "$0")/gpu_lib.sh"
+mkdir -p gpurun_out/prof gpurun_out/pmc
+
+L8B="python bench.py --steps 10 --warmup 3"
+G2="python bench.py --model gpt2_small --seq 1024 --mbs 32 --steps 20 --warmup 5"
+port=29700
+
+torchrun_n() {  # name limit nproc args...
+  local name=$1 lim=$2 n=$3; shift 3; port=$((port + 1))
+  step "$name" "$lim" python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 \
+    --master-port $port "$@"
+}
+
+argsets() {  # tag base-command: one bench per ';'-separated ARGSETS entry (default: the base command once)
+  local tag=$1 base=$2 i=0 a rc
+  IFS=';' read -ra SETS <<< "${ARGSETS:-}"
+  [ ${#SETS[@]} -eq 0 ] && SETS=("")
+  for a in "${SETS[@]}"; do
+    i=$((i + 1))
+    step "${tag}_$i" 400 $base $a || return $?
+    grep -h '"metric"' "gpurun_out/${tag}_$i.log" | sed "s|^|[$a] |" | tee -a "gpurun_out/$tag.jsonl"
+  done
+}
+
+s_tests() {
+  step tests_gpu 900 python -u -m pytest ${SEL:-tests} -m gpu -x -v --timeout 240 --timeout-method thread
+}
+s_smoke() { step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; }
+s_bench() { argsets l8b "$L8B"; }
+s_gpt2() { argsets gpt2 "$G2"; }
+s_check() { s_tests && s_smoke && step bench 400 $L8B && step gpt2 300 $G2; }
+
+s_prof_l8b() {
+  step prof_l8b 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/l8b -o l8b --output-format csv -- \
+    python3 bench.py --steps 2 --warmup 1
+}
+s_prof_gpt2() {
+  step prof_gpt2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/gpt2 -o gpt2 --output-format csv -- \
+    python3 bench.py --model gpt2_small --seq 1024 --mbs 32 --steps 3 --warmup 2
+}
+
+s_pmc_attn() {
+  local prog="python3 tools/bench_kernels.py --only attn --iters 3 --no-sdpa"
+  pmc busy "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS" $prog && \
+  pmc inst "SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_WAVES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_WAIT_INST_ANY" $prog && \
+  pmc grbm "GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD" $prog && \
+  python tools/pmc_summary.py $(find gpurun_out/pmc -name '*counter_collection.csv') > gpurun_out/pmc_summary.txt
+}
+
+s_attn_probe() {
+  local out=gpurun_out/attn_probe.jsonl v envs rep rc
+  : > $out
+  IFS=';' read -ra VS <<< "${VARIANTS:-base}"
+  for rep in 1 2; do
+    for v in "${VS[@]}"; do
+      [ "$v" = "base" ] && envs="" || envs="$v"
+      env $envs KOP_PROBE_TAG="$v" timeout -k 10 120 python tools/attn_probe.py --shapes "${SHAPES:-llama,guide}" \
+        >> $out 2> gpurun_out/attn_probe.err
+      rc=$?; [ $rc -eq 0 ] || { echo "variant '$v' rc=$rc"; tail -5 gpurun_out/attn_probe.err; return $rc; }
+    done
+  done
+  cat $out
+}
+
+rehearse() {  # nproc script args...: the rehearsal's JSON line is appended to gpurun_out/rehearsals.jsonl
+  local n=$1; shift
+  torchrun_n "reh_$((port + 1))" 300 "$n" "$@" && grep -h rehearsal "gpurun_out/reh_$port.log" | tee -a gpurun_out/rehearsals.jsonl
+}
+
+s_dp() {
+  rehearse 2 tools/dp_rehearsal.py --mode zero1 && \
+  rehearse 2 tools/dp_rehearsal.py --mode allreduce && \
+  rehearse 4 tools/dp_rehearsal.py --mode zero1 --accum 4 && \
+  rehearse 4 tools/dp_rehearsal.py --mode zero1 --accum 4 --grad-dtype fp32 && \
+  rehearse 2 tools/dp_rehearsal.py --mode allreduce --accum 2 --grad-dtype fp32 && \
+  rehearse 2 tools/dp_rehearsal.py --mode zero1 --model llama3_1b_proxy --seq 2048 --mbs 1 --bucket-mb 512 && \
+  KOP_DIST_BACKEND=gloo KOP_DEVICE_INDEX=0 torchrun_n bench_dp2 300 2 bench.py --gpus 2 --steps 2 --warmup 1 \
+    --model llama3_1b_proxy --seq 2048
+}
+
+s_tp() {
+  rehearse 2 tools/tp_rehearsal.py --tp 2 --mode zero1 --out /tmp/kop_tp_a && \
+  rehearse 4 tools/tp_rehearsal.py --tp 2 --mode zero1 --out /tmp/kop_tp_b && \
+  rehearse 4 tools/tp_rehearsal.py --tp 2 --mode allreduce --sp 1 --out /tmp/kop_tp_c && \
+  rehearse 4 tools/tp_rehearsal.py --tp 4 --mode zero1 --model llama3_1b_proxy --mbs 1 --out /tmp/kop_tp_d && \
+  KOP_DIST_BACKEND=gloo KOP_DEVICE_INDEX=0 torchrun_n bench_tp2 300 2 bench.py --gpus 2 --tp 2 --steps 2 --warmup 1 \
+    --model llama3_1b_proxy --seq 2048 && \
+  KOP_DIST_BACKEND=gloo KOP_DEVICE_INDEX=0 torchrun_n bench_tp2_sp 300 2 bench.py --gpus 2 --tp 2 --sp 1 --steps 2 \
+    --warmup 1 --model llama3_1b_proxy --seq 2048 && \
+  KOP_DIST_BACKEND=gloo KOP_DEVICE_INDEX=0 torchrun_n tp70b 600 2 bench.py --gpus 2 --tp 2 --model llama3_70b --layers 4 \
+    --recompute 1 --sp 1 --seq 8192 --mbs 1 --accum 1 --steps 2 --warmup 1 --gemm-tuning off
+}
+
+s_wgrad_lag() {
+  step wgrad_tests 600 python -u -m pytest tests/test_wgrad_stream_gpu.py -x -v --timeout 200 --timeout-method thread && (
+    export KOP_WGRAD_STREAM=1 KOP_SIDE_LAG_CYCLES=200000
+    rehearse 2 tools/dp_rehearsal.py --mode zero1 && \
+    rehearse 4 tools/dp_rehearsal.py --mode zero1 --accum 4 && \
+    rehearse 4 tools/dp_rehearsal.py --mode allreduce && \
+    rehearse 2 tools/dp_rehearsal.py --mode zero1 --model tiny_gpt2 --accum 2 && \
+    rehearse 4 tools/tp_rehearsal.py --tp 2 --mode zero1 --sp 1 --out /tmp/kop_tp_lag
+  )
+}
+
+s_wgrad_splitk() {
+  step wgrad_splitk 600 python tools/bench_wgrad_splitk.py ${SPLITK_ARGS:-} && \
+    grep -h '^{' gpurun_out/wgrad_splitk.log > gpurun_out/wgrad_splitk.jsonl
+}
+
+s_tune() {
+  PYTORCH_TUNABLEOP_ROCBLAS_ENABLED=0 KOP_TUNE_MS=100 KOP_TUNE_ITERS=30 step tune 700 python tools/tune_gemms.py && \
+  cp kubeoperator_amd/tuning/tunableop_results_gfx950.csv gpurun_out/ && \
+  step bench_tune_off 600 $L8B --gemm-tuning off && \
+  step bench_tune_use 600 $L8B --gemm-tuning use
+}
+
+s_tune_decode() {
+  KOP_TUNE_MS=60 KOP_TUNE_ITERS=20 step tune_decode 900 python tools/bench_decode.py --batch 1,16,64,128 --prompt 128 \
+    --steps 2 --graph 0 --gemm-tuning tune --gemm-results gpurun_out/tunableop_results_gfx950_decode.csv && \
+  step decode_tuned 400 python tools/bench_decode.py --batch 1,16,64,128 --prompt 2048 --steps 32 --graph 0,1 \
+    --gemm-tuning use --gemm-results gpurun_out/tunableop_results_gfx950_decode.csv
+}
+
+s_serve() {
+  step serve_tests 300 python -u -m pytest tests/test_serve.py -x -v --timeout 120 --timeout-method thread && \
+  step decode 400 python tools/bench_decode.py --batch 1,16,64,128 --prompt 2048 --steps 32 --graph 0,1 && \
+  step serve_bench 500 python tools/bench_serve.py --requests 256 --slots 128 --prompt 256,2048 --new 128
+}
+
+s_fp8() {
+  step fp8_tests 300 python -u -m pytest tests/test_fp8_gpu.py -x -v --timeout 120 --timeout-method thread && \
+  step fp8_bench 400 $L8B --fp8 1
+}
+
+[ $# -gt 0 ] || { sed -n '2,22p' tools/gpu.sh; exit 2; }
+for s in "$@"; do
+  fn="s_${s//-/_}"
+  declare -F "$fn" > /dev/null || { echo "unknown session: $s"; exit 2; }
+  echo "##### session $s $(date +%T)"
+  "$fn" || exit $?
+done

@@ -5,7 +5,8 @@
 set -o pipefail
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+_root="${GRAFT_REPO_ROOT:-$(pwd)}"
+cd /tmp && export TMPDIR=/tmp && cd "$_root"
 step() {
   local name=$1 lim=$2; shift 2
   echo "=== $name $(date +%T)"

@@ -90,6 +90,52 @@ Tensor norm_bwd(const Tensor& dy, const Tensor& s, const Tensor& w, const Tensor
   return dx;
 }
 
+// RMSNorm with the transposed companion: [y, s, rstd, y^T] (s undefined without a residual)
+std::vector<Tensor> rms_norm_fwd_t(const Tensor& x, const c10::optional<Tensor>& residual, const Tensor& w, double eps) {
+  check_bf16(x, "x");
+  check_bf16(w, "weight");
+  TORCH_CHECK(x.is_contiguous() && w.is_contiguous() && x.dim() == 2, "rms_norm_fwd_t: contiguous [rows, H] input");
+  const int H = (int)x.size(1), rows = (int)x.size(0);
+  TORCH_CHECK(kop::rms_norm_t_parts(rows, H) > 0, "rms_norm_fwd_t: H must be 2048 or 4096 and rows a multiple of 16");
+  auto y = at::empty_like(x);
+  auto yt = at::empty({H, rows}, x.options());
+  Tensor s;
+  if (residual.has_value()) {
+    check_bf16(*residual, "residual");
+    TORCH_CHECK(residual->is_contiguous() && residual->sizes() == x.sizes(), "residual shape");
+    s = at::empty_like(x);
+  }
+  auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
+  rc(kop::rms_norm_fwd_t(bp(x), cbp(residual), bp(w), bp(y), s.defined() ? bp(s) : nullptr, bp(yt),
+                         rstd.data_ptr<float>(), rows, H, (float)eps, cur_stream()),
+     "rms_norm_fwd_t");
+  return {y, s, rstd, yt};
+}
+
+// backward: [dx, dx^T]; the weight gradient is written to / accumulated into dw
+std::vector<Tensor> rms_norm_bwd_t(const Tensor& dy, const Tensor& s, const Tensor& w, const Tensor& rstd,
+                                   const c10::optional<Tensor>& dres, const Tensor& dw, bool accumulate) {
+  check_bf16(dy, "dy");
+  check_bf16(s, "s");
+  check_bf16(dw, "dw");
+  TORCH_CHECK(dy.is_contiguous() && s.is_contiguous() && dw.is_contiguous() && s.dim() == 2 && dy.sizes() == s.sizes(),
+              "rms_norm_bwd_t: contiguous [rows, H] inputs");
+  const int H = (int)s.size(1), rows = (int)s.size(0);
+  const int parts = kop::rms_norm_t_parts(rows, H);
+  TORCH_CHECK(parts > 0, "rms_norm_bwd_t: H must be 2048 or 4096 and rows a multiple of 16");
+  if (dres.has_value()) {
+    check_bf16(*dres, "dres");
+    TORCH_CHECK(dres->is_contiguous() && dres->sizes() == s.sizes(), "dres shape");
+  }
+  auto dx = at::empty_like(s);
+  auto dxt = at::empty({H, rows}, s.options());
+  auto part = at::empty({(int64_t)parts * H}, s.options().dtype(at::kFloat));
+  rc(kop::rms_norm_bwd_t(bp(dy), bp(s), bp(w), rstd.data_ptr<float>(), cbp(dres), bp(dx), bp(dxt),
+                         part.data_ptr<float>(), bp(dw), rows, H, accumulate ? 1 : 0, cur_stream()),
+     "rms_norm_bwd_t");
+  return {dx, dxt};
+}
+
 void bias_grad_(const Tensor& dy, const Tensor& db, bool accumulate) {
   check_bf16(dy, "dy");
   check_bf16(db, "db");
@@ -209,6 +255,38 @@ void transpose_(const Tensor& in, const Tensor& out) {
      "transpose (rows and columns must be multiples of 8)");
 }
 
+// RoPE in place on the Q/K heads of x [T, C] fused with out = x^T [C, T] (the attention backward's dQKV)
+void rope_t_(const Tensor& x, const Tensor& cos_t, const Tensor& sin_t, int64_t S, int64_t nheads, int64_t D,
+             bool inverse, const Tensor& out) {
+  check_bf16(x, "x");
+  check_bf16(out, "out");
+  check_rows(x, "x");
+  check_rows(out, "out");
+  check_f32(cos_t, "cos");
+  check_f32(sin_t, "sin");
+  TORCH_CHECK(cos_t.is_contiguous() && sin_t.is_contiguous(), "cos/sin tables must be contiguous");
+  TORCH_CHECK(cos_t.size(-1) == D / 2 && cos_t.size(0) >= S, "cos/sin tables must be [>= S, D/2]");
+  TORCH_CHECK(out.size(0) == x.size(1) && out.size(1) == x.size(0), "out must be [x.cols, x.rows]");
+  rc(kop::rope_transpose(bp(x), bp(out), cos_t.data_ptr<float>(), sin_t.data_ptr<float>(), x.size(0), x.size(1),
+                         x.stride(0), out.stride(0), (int)S, (int)nheads, (int)D, inverse, cur_stream()),
+     "rope_t (head_dim 128 or 64, rows a multiple of 64, columns and rotated columns of 128)");
+}
+
+// ------------------------------------------------------------------ split-K weight-gradient reduction
+// part [S, N, K] fp32 partial planes of one weight gradient -> out [N, K] (bf16 or fp32), overwritten or accumulated
+void splitk_reduce_(const Tensor& part, const Tensor& out, bool accumulate) {
+  check_f32(part, "part");
+  check_gpu(out, "out");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat, "out must be bf16 or fp32");
+  TORCH_CHECK(part.is_contiguous() && out.is_contiguous(), "splitk_reduce: part and out must be contiguous");
+  TORCH_CHECK(part.dim() >= 2 && part.numel() == part.size(0) * out.numel(), "part must be [S, *out.shape]");
+  check_aligned(part, "part");
+  check_aligned(out, "out");
+  rc(kop::splitk_reduce(part.data_ptr<float>(), (int)part.size(0), out.numel(), out.data_ptr(),
+                        out.scalar_type() == at::kFloat, accumulate, cur_stream()),
+     "splitk_reduce (element count must be a multiple of 8)");
+}
+
 // ------------------------------------------------------------------ fp8
 void fp8_quant_(const Tensor& x, const Tensor& out, const Tensor& scale, const Tensor& amax_ws) {
   check_bf16(x, "x");
@@ -313,6 +391,27 @@ void flash_attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const Ten
      "flash_attn_fwd");
 }
 
+// forward that also writes O^T [Hq*D, B*S] (8-wave kernel shapes: S a multiple of 256)
+void flash_attn_fwd_t(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& ot,
+                      const Tensor& lse, int64_t B, int64_t S, int64_t Hq, int64_t Hkv, int64_t D, double scale,
+                      bool causal) {
+  for (auto* t : {&q, &k, &v, &o}) {
+    check_bf16(*t, "q/k/v/o");
+    check_rows(*t, "q/k/v/o");
+    TORCH_CHECK(t->size(0) == B * S, "attention tensors must have B*S rows");
+  }
+  check_bf16(ot, "ot");
+  TORCH_CHECK(ot.is_contiguous() && ot.size(0) == Hq * D && ot.size(1) == B * S, "ot must be a contiguous [Hq*D, B*S]");
+  check_f32(lse, "lse");
+  TORCH_CHECK(lse.numel() == B * Hq * S, "lse size");
+  TORCH_CHECK(q.size(1) >= Hq * D && k.size(1) >= Hkv * D && v.size(1) >= Hkv * D && o.size(1) >= Hq * D,
+              "attention head width");
+  rc(kop::flash_attn_fwd(bp(q), bp(k), bp(v), bp(o), lse.data_ptr<float>(), (int)B, (int)S, (int)Hq, (int)Hkv,
+                         (int)D, q.stride(0), k.stride(0), v.stride(0), o.stride(0), (float)scale, causal,
+                         cur_stream(), bp(ot)),
+     "flash_attn_fwd_t (S must be a multiple of 256)");
+}
+
 int64_t flash_attn_bwd_workspace(int64_t B, int64_t S, int64_t Hq, int64_t D) {
   return (int64_t)kop::flash_attn_bwd_workspace((int)B, (int)S, (int)Hq, (int)D);
 }
@@ -393,6 +492,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("ARCH") = "gfx950";
   m.def("norm_fwd", &norm_fwd);
   m.def("norm_bwd", &norm_bwd);
+  m.def("rms_norm_fwd_t", &rms_norm_fwd_t);
+  m.def("rms_norm_bwd_t", &rms_norm_bwd_t);
   m.def("bias_grad_", &bias_grad_);
   m.def("rope_", &rope_);
   m.def("swiglu_fwd", &swiglu_fwd);
@@ -403,6 +504,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_bwd", &gelu_bwd);
   m.def("cross_entropy_fwd_", &cross_entropy_fwd_);
   m.def("transpose_", &transpose_);
+  m.def("rope_t_", &rope_t_);
+  m.def("splitk_reduce_", &splitk_reduce_);
   m.def("fp8_quant_", &fp8_quant_);
   m.attr("FP8_AMAX_BLOCKS") = kop::kFp8AmaxBlocks;
   m.def("fp8_cast_scaled_", &fp8_cast_scaled_);
@@ -411,6 +514,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_sumsq_", &grad_sumsq_);
   m.def("clip_coef_", &clip_coef_);
   m.def("flash_attn_fwd", &flash_attn_fwd);
+  m.def("flash_attn_fwd_t", &flash_attn_fwd_t);
   m.def("decode_attn", &decode_attn);
   m.def("decode_rope_append_", &decode_rope_append_);
   m.def("flash_attn_bwd_workspace", &flash_attn_bwd_workspace);

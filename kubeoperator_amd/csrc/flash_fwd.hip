@@ -219,7 +219,7 @@ __global__ void __launch_bounds__(512, 1) fa_fwd8_kernel(const bf16_t* __restric
                                                          const bf16_t* __restrict__ v, bf16_t* __restrict__ o,
                                                          float* __restrict__ lse, int B, int S, int Hq, int Hkv,
                                                          int64_t qs, int64_t ks, int64_t vs, int64_t os,
-                                                         float scale_log2, int causal) {
+                                                         float scale_log2, int causal, bf16_t* __restrict__ ot) {
   constexpr int NW = 8, BM = 256, BN = 64, ROWB = D * 2;
   constexpr int TILE = BN * ROWB;
   constexpr int NSLOT = STAGGER ? 4 : 3;
@@ -428,6 +428,19 @@ __global__ void __launch_bounds__(512, 1) fa_fwd8_kernel(const bf16_t* __restric
   const float lt = l + __shfl_xor(l, 32, 64);
   const float inv = 1.f / lt;
   if (hh == 0) lse[((int64_t)(b * Hq + hq)) * S + q0w + r] = (m + __log2f(lt)) * 0.69314718056f;
+  if (ot != nullptr) {
+    // O^T [Hq*D, B*S] as well: the K-contiguous X operand of the Wo weight-gradient GEMM. Lane r holds one
+    // token of every column it owns, so a column's 32 tokens of the wave are one 64-B segment (the two waves of
+    // a 128-B line are in this workgroup and merge in L2); rounded exactly like O.
+    const int64_t T = (int64_t)B * S;
+    bf16_t* otp = ot + (int64_t)(hq * D + 4 * hh) * T + (int64_t)b * S + q0w + r;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) otp[(int64_t)(dt * 32 + 8 * g + i) * T] = f2bf(oacc[dt][4 * g + i] * inv);
+  }
   // widened store tail (guide T21): lane r holds columns 8g..8g+3 of row r, lane r+32 columns 8g+4..8g+7; one
   // v_permlane32_swap per dword of a (g, g+1) pair leaves lane r with columns 16p..16p+7 and lane r+32 with
   // 16p+8..16p+15, so each lane writes 16 B per pair: 8 dwordx4 stores instead of 16 dwordx2
@@ -451,7 +464,7 @@ __global__ void __launch_bounds__(512, 1) fa_fwd8_kernel(const bf16_t* __restric
 template <int D, bool STAGGER, bool PK = false>
 static void launch_fwd8(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int S,
                         int Hq, int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t os, float sl2, bool causal,
-                        hipStream_t stream) {
+                        hipStream_t stream, bf16_t* ot) {
   const size_t lds = (STAGGER ? 4 : 3) * 2 * 64 * (D * 2);
   static bool attr = false;
   if (!attr) {
@@ -460,7 +473,8 @@ static void launch_fwd8(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_
     attr = true;
   }
   const int grid = B * Hq * (S / 256);
-  fa_fwd8_kernel<D, STAGGER, PK><<<grid, 512, lds, stream>>>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal);
+  fa_fwd8_kernel<D, STAGGER, PK><<<grid, 512, lds, stream>>>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal,
+                                                             ot);
 }
 
 constexpr int kFwdWaves = 4;
@@ -482,7 +496,7 @@ static void launch_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t
 
 int flash_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int S, int Hq,
                    int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, float scale, bool causal,
-                   hipStream_t stream) {
+                   hipStream_t stream, bf16_t* ot) {
   if (S % (32 * kFwdWaves) != 0 || Hq % Hkv != 0) return -1;
   if (qs % 8 || ks % 8 || vs % 8 || os % 8) return -2;
   const float sl2 = scale * 1.4426950408889634f;
@@ -492,16 +506,17 @@ int flash_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o,
   }();
   if (S % 256 == 0 && variant >= 8) {
     if (D == 128) {
-      if (variant == 9) launch_fwd8<128, true>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
-      else if (variant == 10) launch_fwd8<128, false, true>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
-      else launch_fwd8<128, false>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
+      if (variant == 9) launch_fwd8<128, true>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream, ot);
+      else if (variant == 10) launch_fwd8<128, false, true>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream, ot);
+      else launch_fwd8<128, false>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream, ot);
     } else if (D == 64) {
-      if (variant == 9) launch_fwd8<64, true>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
-      else if (variant == 10) launch_fwd8<64, false, true>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
-      else launch_fwd8<64, false>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
+      if (variant == 9) launch_fwd8<64, true>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream, ot);
+      else if (variant == 10) launch_fwd8<64, false, true>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream, ot);
+      else launch_fwd8<64, false>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream, ot);
     } else return -3;
     return 0;
   }
+  if (ot != nullptr) return -4;  // O^T only from the 8-wave kernel
   if (D == 128) launch_fwd<128>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
   else if (D == 64) launch_fwd<64>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream);
   else return -3;

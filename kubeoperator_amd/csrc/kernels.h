@@ -13,6 +13,13 @@ typedef uint16_t bf16_t;
 int norm_fwd(const bf16_t* x, const bf16_t* r, const bf16_t* w, const bf16_t* b, bf16_t* y, bf16_t* s_out, float* rstd,
              float* mean, int rows, int H, float eps, bool layernorm, hipStream_t stream);
 int norm_bwd_partial_rows(int rows, int H);
+// RMSNorm writing the transposed companion ([H, rows]) of its output (forward) / input gradient (backward)
+int rms_norm_t_parts(int rows, int H);  // 0: shape not supported
+int rms_norm_fwd_t(const bf16_t* x, const bf16_t* r, const bf16_t* w, bf16_t* y, bf16_t* s_out, bf16_t* yt, float* rstd,
+                   int rows, int H, float eps, hipStream_t stream);
+int rms_norm_bwd_t(const bf16_t* dy, const bf16_t* s, const bf16_t* w, const float* rstd, const bf16_t* dres,
+                   bf16_t* dx, bf16_t* dxt, float* part, bf16_t* dw, int rows, int H, int accumulate,
+                   hipStream_t stream);
 int norm_bwd(const bf16_t* dy, const bf16_t* s, const bf16_t* w, const float* rstd, const float* mean,
              const bf16_t* dres, bf16_t* dx, float* part, bf16_t* dw, bf16_t* db, int rows, int H, bool layernorm,
              int accumulate, hipStream_t stream);
@@ -45,6 +52,10 @@ int clip_coef(const float* sumsq, float max_norm, float* coef, float* norm_out, 
 
 // transpose.hip
 int transpose2d(const bf16_t* in, bf16_t* out, int64_t R, int64_t C, int64_t ldi, int64_t ldo, hipStream_t stream);
+// RoPE in place on the first nheads heads (D = 128) + transpose of the whole [R, C] matrix into out [C, R]
+int rope_transpose(bf16_t* x, bf16_t* out, const float* cos_t, const float* sin_t, int64_t R, int64_t C, int64_t ldx,
+                   int64_t ldo, int S, int nheads, int D, bool inverse, hipStream_t stream);
+int splitk_reduce(const float* part, int S, int64_t n, void* out, bool out_f32, bool accumulate, hipStream_t stream);
 
 // fp8.hip: per-tensor OCP E4M3 quantization (current scaling): out = rne(clamp(x / scale)), scale = amax / 448;
 // partial_ws: kFp8AmaxBlocks floats of scratch
@@ -58,7 +69,7 @@ int fp8_transpose_cast(const bf16_t* in, uint8_t* out, int64_t R, int64_t C, int
 // flash_attn.hip
 int flash_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int S, int Hq,
                    int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, float scale, bool causal,
-                   hipStream_t stream);
+                   hipStream_t stream, bf16_t* ot = nullptr);
 size_t flash_attn_bwd_workspace(int B, int S, int Hq, int D);
 // dQ algorithm: 10 = from the materialised dS (default), 9 = recompute S/dP (8-wave, staggered),
 // 8 = lockstep, <8 = 4-wave.

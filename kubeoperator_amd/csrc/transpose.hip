@@ -118,6 +118,101 @@ __global__ void __launch_bounds__(256) transpose_wide_kernel(const bf16_t* __res
   }
 }
 
+// RoPE (in place, on the first `rope_cols` columns = the Q and K heads of a fused-QKV row matrix, head_dim 128 / 64)
+// fused with the transpose of the WHOLE matrix: the attention backward's dQ|dK|dV leaves the flash kernels
+// un-rotated; this applies the inverse rotation (sign = -1) and also writes dQKV^T, the K-contiguous dY operand of
+// the QKV weight-gradient GEMM, in the same pass (the separate rope + transpose read dQKV twice more).
+// Tiles as transpose_wide_kernel<true> (64 rows x 128 columns = one or two heads); a rotary pair (d, d + D/2) sits
+// in lanes t and t ^ (D/16) of one wave: the partner half comes by a lane swap.
+template <int D>
+__global__ void __launch_bounds__(256) rope_t_kernel(bf16_t* __restrict__ x, bf16_t* __restrict__ out,
+                                                     const float* __restrict__ cos_t, const float* __restrict__ sin_t,
+                                                     int64_t R, int64_t C, int64_t ldx, int64_t ldo, int S,
+                                                     int64_t rope_cols, float sign) {
+  constexpr int TR = 64, TC = 128, P = 65, HALF = D / 2, PX = HALF / 8;  // PX: lane distance of a rotary pair
+  __shared__ uint32_t lds[TR * P];
+  const int t = threadIdx.x;
+  const int64_t tiles_r = R / TR;
+  const int64_t tr = blockIdx.x % tiles_r, tc = blockIdx.x / tiles_r;
+  const int64_t r0 = tr * TR, c0 = tc * TC;
+  const int ch = t & 15;
+  u32x4 v[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int row = p * 16 + (t >> 4);
+    v[p] = *reinterpret_cast<const u32x4*>(x + (r0 + row) * ldx + c0 + ch * 8);
+  }
+  if (c0 < rope_cols) {  // block-uniform: a Q or K head
+    const bool lo_half = (ch & PX) == 0;
+    const int j = (ch & (PX - 1)) * 8;  // rotary pair index of this lane's first column
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int row = p * 16 + (t >> 4);
+      const int pos = (int)((r0 + row) % S);
+      u32x4 pv;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pv[i] = (uint32_t)__shfl_xor((int)v[p][i], PX, 64);
+      const f32x4* cp = reinterpret_cast<const f32x4*>(cos_t + (int64_t)pos * HALF + j);
+      const f32x4* sp = reinterpret_cast<const f32x4*>(sin_t + (int64_t)pos * HALF + j);
+      const f32x4 c0v = cp[0], c1v = cp[1], s0v = sp[0], s1v = sp[1];
+      float mine[8], other[8], o[8];
+      unpack8(v[p], mine);
+      unpack8(pv, other);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float c = i < 4 ? c0v[i] : c1v[i - 4];
+        const float sn = (i < 4 ? s0v[i] : s1v[i - 4]) * sign;
+        // (a, b) = (x_d, x_{d+64}) -> (a c - b s, b c + a s)
+        o[i] = lo_half ? mine[i] * c - other[i] * sn : mine[i] * c + other[i] * sn;
+      }
+      v[p] = pack8(o);
+      *reinterpret_cast<u32x4*>(x + (r0 + row) * ldx + c0 + ch * 8) = v[p];
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    uint32_t* d = lds + (p * 16 + (t >> 4)) * P + ch * 4;
+    d[0] = v[p][0];
+    d[1] = v[p][1];
+    d[2] = v[p][2];
+    d[3] = v[p][3];
+  }
+  __syncthreads();
+  const int chunk = t & 7;
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int pair = (t >> 3) + 32 * jj;
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = lds[(chunk * 8 + i) * P + pair];
+    u32x4 lo, hi;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      lo[i] = (w[2 * i] & 0xffffu) | (w[2 * i + 1] << 16);
+      hi[i] = (w[2 * i] >> 16) | (w[2 * i + 1] & 0xffff0000u);
+    }
+    const int64_t oc = c0 + 2 * pair, orr = r0 + chunk * 8;
+    *reinterpret_cast<u32x4*>(out + oc * ldo + orr) = lo;
+    *reinterpret_cast<u32x4*>(out + (oc + 1) * ldo + orr) = hi;
+  }
+}
+
+int rope_transpose(bf16_t* x, bf16_t* out, const float* cos_t, const float* sin_t, int64_t R, int64_t C, int64_t ldx,
+                   int64_t ldo, int S, int nheads, int D, bool inverse, hipStream_t stream) {
+  if ((D != 128 && D != 64) || R % 64 != 0 || C % 128 != 0 || ldx % 8 != 0 || ldo % 8 != 0 ||
+      (int64_t)nheads * D > C || ((int64_t)nheads * D) % 128 != 0)
+    return -1;
+  const int64_t n = (R / 64) * (C / 128);
+  if (n == 0) return 0;
+  if (n > 0x7fffffff) return -2;
+  const float sign = inverse ? -1.f : 1.f;
+  if (D == 128)
+    rope_t_kernel<128><<<(unsigned)n, 256, 0, stream>>>(x, out, cos_t, sin_t, R, C, ldx, ldo, S, (int64_t)nheads * D, sign);
+  else
+    rope_t_kernel<64><<<(unsigned)n, 256, 0, stream>>>(x, out, cos_t, sin_t, R, C, ldx, ldo, S, (int64_t)nheads * D, sign);
+  return 0;
+}
+
 namespace {
 int transpose_mode() {
   static const int mode = [] {

@@ -51,8 +51,12 @@ class LlamaBlock(nn.Module):
         self.w_gate_up = nn.Parameter(torch.empty(2 * self.ffn, H))
         self.w_down = nn.Parameter(torch.empty(H, self.ffn))
 
-    def forward(self, x, pending, cos, sin, B, S):
+    def forward(self, x, pending, cos, sin, B, S, box_in=None, box_out=None):
+        """``box_in`` / ``box_out`` (``kf.TBox``, set by ``Llama.forward`` when the transposed companions are on):
+        the norms write y^T / dx^T for the weight gradients of the projections around them."""
         c, tp = self.cfg, self.tp
+        if box_out is not None:
+            return self._forward_t(x, pending, cos, sin, B, S, box_in, box_out)
         if pending is None:
             y, x1 = kf.rms_norm(x, self.attn_norm, c.norm_eps), x
         else:
@@ -68,6 +72,26 @@ class LlamaBlock(nn.Module):
         a = reduce_from_tp(kf.linear(a, self.wo), tp)
         y2, x2 = kf.rms_norm(x1, self.mlp_norm, c.norm_eps, residual=a)
         return x2, reduce_from_tp(kf.swiglu_mlp(y2, self.w_gate_up, self.w_down, tp_group=g), tp)
+
+    def _forward_t(self, x, pending, cos, sin, B, S, box_in, box_out):
+        """One GPU rank, no TP: the forward norms hand y^T to the QKV / gate|up projections (``xt``), the backward
+        norms hand dx^T to the Wo / W_down projections, the attention backward hands dQKV^T (fused with its
+        inverse RoPE) to the QKV projection (``box``) and the attention forward hands O^T to Wo (``xt``): none of the
+        block's weight-gradient GEMMs transposes an operand (csrc/norms.hip rms_fwd_t / rms_bwd_t,
+        csrc/transpose.hip rope_t, csrc/flash_fwd.hip O^T tail)."""
+        c = self.cfg
+        if pending is None:
+            (y, yt), x1 = kf.rms_norm(x, self.attn_norm, c.norm_eps, want_t=True), x
+        else:
+            y, x1, yt = kf.rms_norm(x, self.attn_norm, c.norm_eps, residual=pending, want_t=True, box=box_in)
+        box_qkv = kf.TBox()
+        qkv = kf.linear(y, self.wqkv, xt=yt, box=box_qkv)
+        a, at = kf.rope_attention(qkv, cos, sin, B, S, self.hq, self.hkv, c.head_dim, causal=True, box=box_qkv,
+                                  want_ot=True)
+        box_wo = kf.TBox()
+        a = kf.linear(a, self.wo, xt=at, box=box_wo)
+        y2, x2, yt2 = kf.rms_norm(x1, self.mlp_norm, c.norm_eps, residual=a, want_t=True, box=box_wo)
+        return x2, kf.swiglu_mlp(y2, self.w_gate_up, self.w_down, xt=yt2, box=box_out)
 
 
 class Llama(nn.Module):
@@ -119,6 +143,12 @@ class Llama(nn.Module):
             self._rope[key] = rope_cache(S, self.cfg.head_dim, self.cfg.rope_theta, device=device)
         return self._rope[key]
 
+    def _companions(self, x) -> bool:
+        """Norm kernels with transposed outputs: one rank of the block projections (no TP), bf16 GEMMs (the FP8
+        path transposes while casting), H 2048 / 4096 and T a multiple of 16 (``kf.norm_t_enabled``)."""
+        return (x.is_cuda and torch.is_grad_enabled() and not self.tp.enabled and kf.norm_t_enabled()
+                and getattr(self.layers[0].wqkv, "w8", None) is None and kf._t_ok(x))
+
     def forward(self, ids: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
         B, S = ids.shape
         cos, sin = self.rope_tables(S, ids.device)
@@ -128,12 +158,16 @@ class Llama(nn.Module):
             ids, targets = ids[rows], targets[rows]
         x = kf.embedding(ids, self.tok_emb)
         pending = None
-        for blk in self.layers:
+        # transposed companions of the norms (see LlamaBlock._forward_t): one box per block for its MLP output
+        boxes = [kf.TBox() for _ in self.layers] if self._companions(x) else [None] * len(self.layers)
+        box_in = None
+        for blk, box in zip(self.layers, boxes):
             if self.recompute and torch.is_grad_enabled():
                 # keep only the block's inputs; its activations are rebuilt in backward (long sequences)
-                x, pending = checkpoint(blk, x, pending, cos, sin, B, S, use_reentrant=False)
+                x, pending = checkpoint(blk, x, pending, cos, sin, B, S, box_in, box, use_reentrant=False)
             else:
-                x, pending = blk(x, pending, cos, sin, B, S)
-        y, _ = kf.rms_norm(x, self.final_norm, self.cfg.norm_eps, residual=pending)
+                x, pending = blk(x, pending, cos, sin, B, S, box_in, box)
+            box_in = box
+        y, _ = kf.rms_norm(x, self.final_norm, self.cfg.norm_eps, residual=pending, box=box_in)
         head = self.tok_emb if self.cfg.tie_embeddings else self.lm_head
         return kf.cross_entropy_lmhead(y, head, targets)

@@ -195,12 +195,48 @@ def _dx8(dy2, w):
     return fp8.mm8(dy8, sdy, w.wt8.t(), w.wt8_scale, out_dtype=dy2.dtype), dy2, sdy
 
 
+# Narrow weight gradients (GPT-2-small: 768 x 768 ... 3072 x 768 over T = 32768 rows) are a few dozen 256 x 256
+# output tiles for 256 CUs: split the token rows into s chunks as ONE batched GEMM with fp32 outputs, then fold
+# the partial planes into the gradient with one HIP pass (csrc/splitk.hip). s doubles while s x tiles stays
+# within half the CUs' worth of tiles, up to 16; at Llama widths (>= 256 tiles) s = 1. One MI355X
+# (profiles/r3_wgrad_splitk_probe.jsonl): proj 0.124 -> 0.059 ms, qkv 0.230 -> 0.155, out 0.232 -> 0.176.
+_DW_SPLITK = os.environ.get("KOP_DW_SPLITK", "auto")  # auto | off | fixed split count
+_DW_SPLITK_MIN_ROWS = 1024  # rows per chunk
+
+
+def _splitk(T: int, N: int, K: int) -> int:
+    if _DW_SPLITK == "off":
+        return 1
+    if _DW_SPLITK.isdigit():
+        s = int(_DW_SPLITK)
+    else:
+        tiles = -(-N // 256) * -(-K // 256)
+        s = 1
+        while s < 16 and tiles * s * 2 <= 256:
+            s *= 2
+    while s > 1 and (T % s or T // s < _DW_SPLITK_MIN_ROWS or (T // s) % 8):
+        s //= 2
+    return s
+
+
+def _dw_splitk_into(dy2, x2, out, accumulate, s):
+    T, N = dy2.shape
+    c = T // s
+    part = torch.bmm(dy2.view(s, c, N).transpose(1, 2), x2.view(s, c, x2.shape[1]), out_dtype=torch.float32)
+    _lib().splitk_reduce_(part, out, accumulate)
+
+
 def _dw_into(dy2, x2, out, accumulate):
     """out (+)= dy2^T @ x2, the reduction running over the token rows."""
     wide = min(dy2.shape[1], x2.shape[1]) >= _DW_TN_MIN_WIDTH
     if ((_DW_LAYOUT == "tn" or (_DW_LAYOUT == "auto" and wide)) and dy2.shape[0] >= _DW_TN_MIN_ROWS
             and dy2.shape[0] % 8 == 0 and _rows_ok(dy2) and _rows_ok(x2)):
         _mm_into(transpose(dy2), transpose(x2).t(), out, accumulate)
+        return
+    s = _splitk(dy2.shape[0], dy2.shape[1], x2.shape[1])
+    if (s > 1 and dy2.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and dy2.is_contiguous()
+            and x2.is_contiguous() and out.is_contiguous() and out.numel() % 8 == 0):
+        _dw_splitk_into(dy2, x2, out, accumulate, s)
     else:
         _mm_into(dy2.t(), x2, out, accumulate)
 
@@ -234,9 +270,20 @@ def _tp_reduce_async(dx, group):
     return dist.all_reduce(dx, group=group, async_op=True)
 
 
+def _dw_t_into(dy2, x2, xt, dyt, out, acc):
+    """dW (+)= dY^T X with either K-contiguous operand possibly supplied by its producer (``xt`` = X^T from the
+    norm forward, ``dyt`` = dY^T from the norm backward); the missing one is transposed here."""
+    if dyt is None:
+        dyt = transpose(dy2) if _rows_ok(dy2) else None
+    if dyt is None:
+        _mm_into(dy2.t(), xt.t() if xt is not None else x2, out, acc)
+        return
+    _mm_into(dyt, xt.t() if xt is not None else (transpose(x2).t() if _rows_ok(x2) else x2), out, acc)
+
+
 class _Linear(Function):
     @staticmethod
-    def forward(ctx, x, w, b, tp_group=None):
+    def forward(ctx, x, w, b, tp_group=None, xt=None, box=None):
         x2 = x.reshape(-1, x.shape[-1])
         ctx.tp_group = tp_group
         ctx.sx = None
@@ -244,17 +291,21 @@ class _Linear(Function):
             y = torch.addmm(b, x2, w.t())
         else:
             y, ctx.sx = _fwd8(x2, w)
-        ctx.save_for_backward(x2, w)
+        ctx.has_xt = xt is not None and ctx.sx is None
+        # with X^T from the producer only X^T is kept for backward (the same bytes as X)
+        ctx.save_for_backward(xt if ctx.has_xt else x2, w)
         ctx.has_b = b is not None
         if b is not None:
             ctx.b = b
         ctx.in_shape = x.shape
+        ctx.box = box
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
         x2, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, w.shape[0])
+        dyt = ctx.box.take(dy2) if ctx.box is not None else None
         if _fp8_bwd(w, ctx.sx):
             from . import fp8
 
@@ -267,22 +318,32 @@ class _Linear(Function):
                        dy2, x2, sdy, sx) if ctx.needs_input_grad[1] else None
             if work is not None:
                 work.wait()
-            return dx, dw, None, None
+            return dx, dw, None, None, None, None
         dx = _dx(dy2, w) if ctx.needs_input_grad[0] else None
         work = _tp_reduce_async(dx, ctx.tp_group)
         dx = dx.view(ctx.in_shape) if dx is not None else None
-        dw = _sink(w, lambda out, acc: _dw_into(dy2, x2, out, acc), dy2, x2) if ctx.needs_input_grad[1] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            if ctx.has_xt or dyt is not None:
+                xt = x2 if ctx.has_xt else None
+                xr = None if ctx.has_xt else x2
+                dw = _sink(w, lambda out, acc: _dw_t_into(dy2, xr, xt, dyt, out, acc),
+                           *[t for t in (dy2, x2, dyt) if t is not None])
+            else:
+                dw = _sink(w, lambda out, acc: _dw_into(dy2, x2, out, acc), dy2, x2)
         db = None
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = _sink(ctx.b, lambda out, acc: _bias_grad_into(dy2, out, acc), dy2)
         if work is not None:
             work.wait()
-        return dx, dw, db, None
+        return dx, dw, db, None, None, None
 
 
-def linear(x, w, b=None, tp_group=None):
+def linear(x, w, b=None, tp_group=None, xt=None, box=None):
     """``tp_group``: ``w`` is a column shard of a tensor-parallel projection (``parallel.tensor``) whose input is
-    replicated over the group; the input gradient is summed over it, overlapped with the weight gradient."""
+    replicated over the group; the input gradient is summed over it, overlapped with the weight gradient.
+    ``xt``: X^T from the producer of ``x`` (``rms_norm(want_t=True)``); ``box``: a ``TBox`` that the consumer of
+    the output fills with dY^T in backward (``rms_norm(box=)``). Both feed the weight-gradient GEMM."""
     if not x.is_cuda:
         if tp_group is not None:
             from ..parallel.tensor import _CopyToTP
@@ -290,37 +351,84 @@ def linear(x, w, b=None, tp_group=None):
             x = _CopyToTP.apply(x, tp_group)
         return F.linear(x, w, b)
     _gate(w, b)
-    return _Linear.apply(x, w, b, tp_group)
+    return _Linear.apply(x, w, b, tp_group, xt, box)
 
 
 # ---------------------------------------------------------------------------------------------------
 # RMSNorm / LayerNorm with fused residual add
 # ---------------------------------------------------------------------------------------------------
+class TBox:
+    """Hands the transposed copy of a gradient from the autograd node that produced it to the node that consumes it
+    as dY (the model creates one per producer / consumer pair in forward). The norm backward fills it
+    (``rms_norm_bwd_t``), the projection's backward takes it for its weight-gradient GEMM. ``take`` returns it
+    only for the very tensor that was put -- same storage, shape and version: if autograd summed another
+    contribution into the gradient in place, or handed the consumer a new tensor, the consumer transposes as
+    before."""
+
+    __slots__ = ("t", "key")
+
+    def __init__(self):
+        self.t = None
+        self.key = None
+
+    def put(self, g, gt):
+        self.t, self.key = gt, (g.data_ptr(), tuple(g.shape), g._version)
+
+    def take(self, g):
+        t, key = self.t, self.key
+        self.t = self.key = None
+        if t is not None and key == (g.data_ptr(), tuple(g.shape), g._version):
+            return t
+        return None
+
+
+_NORM_T = os.environ.get("KOP_NORM_T", "1") != "0"
+
+
+def norm_t_enabled() -> bool:
+    """Transposed-companion norms on (``KOP_NORM_T=0`` turns them off: the projections transpose as before)."""
+    return _NORM_T and _DW_LAYOUT != "nt"
+
+
+def _t_ok(x2) -> bool:
+    """Shapes the transposed-companion RMSNorm kernels take (csrc/norms.hip rms_fwd_t / rms_bwd_t)."""
+    return x2.dim() == 2 and x2.shape[1] in (2048, 4096) and x2.shape[0] % 16 == 0 and x2.shape[0] >= _DW_TN_MIN_ROWS
+
+
 class _Norm(Function):
     @staticmethod
-    def forward(ctx, x, residual, w, b, eps, layernorm):
+    def forward(ctx, x, residual, w, b, eps, layernorm, want_t=False, box=None):
         lib = _lib()
         x = x.contiguous()
-        y, s, rstd, mean = lib.norm_fwd(x, residual.contiguous() if residual is not None else None, w, b, eps, layernorm)
         has_res = residual is not None
+        yt = None
+        if want_t:
+            y, s, rstd, yt = lib.rms_norm_fwd_t(x, residual.contiguous() if has_res else None, w, eps)
+            mean = None
+            ctx.mark_non_differentiable(yt)
+            ctx.set_materialize_grads(False)  # no zero-filled [H, T] "gradient" of y^T
+        else:
+            y, s, rstd, mean = lib.norm_fwd(x, residual.contiguous() if has_res else None, w, b, eps, layernorm)
         if not has_res:
             s = x
         ctx.save_for_backward(s, w, rstd, mean if layernorm else None)
         ctx.layernorm = layernorm
         ctx.has_res = has_res
         ctx.b = b
-        if has_res:
-            return y, s
-        return y
+        ctx.box = box
+        ctx.want_t = want_t
+        out = (y, s) if has_res else (y,)
+        if want_t:
+            out = out + (yt,)
+        return out if len(out) > 1 else y
 
     @staticmethod
-    def backward(ctx, dy, ds_extra=None):
+    def backward(ctx, dy, *rest):
         lib = _lib()
         s, w, rstd, mean = ctx.saved_tensors
+        ds_extra = rest[0] if ctx.has_res else None
         dy = dy.contiguous()
         dres = ds_extra.contiguous() if ds_extra is not None else None
-        dw_holder = {}
-        db_holder = {}
 
         b = ctx.b
         need_w = ctx.needs_input_grad[2]
@@ -333,7 +441,12 @@ class _Norm(Function):
         if ctx.layernorm:
             db_buf = mg_b if (mg_b is not None and not staged) else torch.empty_like(b)
         acc = w._kop_hooks.accumulate_for(w) if mg_w is not None else False
-        dx = lib.norm_bwd(dy, s, w, rstd, mean, dres, dw_buf, db_buf, ctx.layernorm, acc and not staged)
+        if ctx.box is not None and not ctx.layernorm and _t_ok(s):
+            # also write dx^T: the dY operand of the weight gradient of the projection that produced x
+            dx, dxt = lib.rms_norm_bwd_t(dy, s, w, rstd, dres, dw_buf, acc and not staged)
+            ctx.box.put(dx, dxt)
+        else:
+            dx = lib.norm_bwd(dy, s, w, rstd, mean, dres, dw_buf, db_buf, ctx.layernorm, acc and not staged)
         if staged:
             for mg, buf in ((mg_w, dw_buf), (mg_b, db_buf)):
                 if mg is not None and buf is not None:
@@ -350,18 +463,27 @@ class _Norm(Function):
                 b._kop_hooks.ready(b)
             else:
                 db = db_buf
-        del dw_holder, db_holder
         dres_out = dx if ctx.has_res else None
-        return dx, dres_out, dw, db, None, None
+        return dx, dres_out, dw, db, None, None, None, None
 
 
-def rms_norm(x, w, eps=1e-5, residual=None):
-    """y = rmsnorm(x (+ residual)) * w; returns y, or (y, x + residual) when residual is given."""
+def rms_norm(x, w, eps=1e-5, residual=None, want_t=False, box=None):
+    """y = rmsnorm(x (+ residual)) * w; returns y, or (y, x + residual) when residual is given.
+
+    ``want_t``: also return y^T ([H, T], last in the tuple; None where the kernel does not take the shape), the
+    X operand of the next projection's weight-gradient GEMM (``linear(..., xt=)``). ``box`` (a ``TBox``): the
+    backward also writes dx^T into it, for the projection whose output is ``x`` / ``residual``."""
     if not x.is_cuda:
         y, s = ref.rms_norm_ref(x, w, eps, residual)
-        return (y, s) if residual is not None else y
+        out = (y, s) if residual is not None else (y,)
+        out = out + (None,) if want_t else out
+        return out if len(out) > 1 else y
     _gate(w)
-    return _Norm.apply(x, residual, w, None, eps, False)
+    t = bool(want_t) and _t_ok(x.reshape(-1, x.shape[-1]))
+    out = _Norm.apply(x, residual, w, None, eps, False, t, box)
+    if want_t and not t:
+        out = (out if isinstance(out, tuple) else (out,)) + (None,)
+    return out
 
 
 def layer_norm(x, w, b, eps=1e-5, residual=None):
@@ -369,7 +491,7 @@ def layer_norm(x, w, b, eps=1e-5, residual=None):
         y, s = ref.layer_norm_ref(x, w, b, eps, residual)
         return (y, s) if residual is not None else y
     _gate(w, b)
-    return _Norm.apply(x, residual, w, b, eps, True)
+    return _Norm.apply(x, residual, w, b, eps, True, False, None)
 
 
 # ---------------------------------------------------------------------------------------------------
@@ -455,7 +577,7 @@ class _SwiGLUMLP(Function):
     so neither h nor dgu is transposed separately."""
 
     @staticmethod
-    def forward(ctx, x, w_gu, w_d, tp_group=None):
+    def forward(ctx, x, w_gu, w_d, tp_group=None, xt=None, box=None):
         lib = _lib()
         x2 = x.reshape(-1, x.shape[-1])
         ctx.tp_group = tp_group
@@ -468,9 +590,12 @@ class _SwiGLUMLP(Function):
         else:
             h = lib.swiglu_fwd(gu)
         y, ctx.sh = _fwd8(h, w_d)
-        ctx.save_for_backward(x2, w_gu, w_d, gu, ht if ht is not None else h)
+        # X^T from the norm forward replaces X (only the gate|up weight gradient reads it; the FP8 path keeps X)
+        ctx.has_xt = xt is not None and ctx.sx is None
+        ctx.save_for_backward(xt if ctx.has_xt else x2, w_gu, w_d, gu, ht if ht is not None else h)
         ctx.has_ht = ht is not None
         ctx.in_shape = x.shape
+        ctx.box = box
         return y.view(*x.shape[:-1], w_d.shape[0])
 
     @staticmethod
@@ -479,18 +604,20 @@ class _SwiGLUMLP(Function):
         x2, w_gu, w_d, gu, h_or_ht = ctx.saved_tensors
         T, F2 = gu.shape
         dy2 = dy.reshape(-1, w_d.shape[0])
+        dyt = ctx.box.take(dy2) if ctx.box is not None else None
         if ctx.has_ht and _fp8_bwd(w_d, ctx.sh) and _fp8_bwd(w_gu, ctx.sx):
             return _SwiGLUMLP._backward_fp8(ctx, lib, x2, w_gu, w_d, gu, h_or_ht, dy2)
         dh = _dx(dy2, w_d)
         dw_d = None
         if ctx.needs_input_grad[2]:
             if ctx.has_ht:
-                a = transpose(dy2) if _rows_ok(dy2) else dy2.t()
+                a = dyt if dyt is not None else (transpose(dy2) if _rows_ok(dy2) else dy2.t())
                 dw_d = _sink(w_d, lambda out, acc: _mm_into(a, h_or_ht.t(), out, acc), a, h_or_ht)
             else:
                 dw_d = _sink(w_d, lambda out, acc: _dw_into(dy2, h_or_ht, out, acc), dy2, h_or_ht)
         dh = dh.contiguous()
-        if _SWIGLU_T and (F2 // 2) % 64 == 0 and _tn_ok(T, F2, x2.shape[1]) and _rows_ok(x2):
+        H = x2.shape[0] if ctx.has_xt else x2.shape[1]
+        if _SWIGLU_T and (F2 // 2) % 64 == 0 and _tn_ok(T, F2, H) and (ctx.has_xt or _rows_ok(x2)):
             dgu, dgut = lib.swiglu_bwd_t(gu, dh)
         else:
             dgu, dgut = lib.swiglu_bwd(gu, dh), None
@@ -499,13 +626,18 @@ class _SwiGLUMLP(Function):
         dx = dx.view(ctx.in_shape) if dx is not None else None
         dw_gu = None
         if ctx.needs_input_grad[1]:
-            if dgut is not None:
+            if ctx.has_xt:
+                if dgut is not None:
+                    dw_gu = _sink(w_gu, lambda out, acc: _mm_into(dgut, x2.t(), out, acc), dgut, x2)
+                else:
+                    dw_gu = _sink(w_gu, lambda out, acc: _mm_into(dgu.t(), x2.t(), out, acc), dgu, x2)
+            elif dgut is not None:
                 dw_gu = _sink(w_gu, lambda out, acc: _mm_into(dgut, transpose(x2).t(), out, acc), dgut, x2)
             else:
                 dw_gu = _sink(w_gu, lambda out, acc: _dw_into(dgu, x2, out, acc), dgu, x2)
         if work is not None:
             work.wait()
-        return dx, dw_gu, dw_d, None
+        return dx, dw_gu, dw_d, None, None, None
 
 
     @staticmethod
@@ -533,13 +665,14 @@ class _SwiGLUMLP(Function):
                           dgut, x2, sdgu, sx)
         if work is not None:
             work.wait()
-        return dx.view(ctx.in_shape) if ctx.needs_input_grad[0] else None, dw_gu, dw_d, None
+        return dx.view(ctx.in_shape) if ctx.needs_input_grad[0] else None, dw_gu, dw_d, None, None, None
 
 
-def swiglu_mlp(x, w_gu, w_d, tp_group=None):
+def swiglu_mlp(x, w_gu, w_d, tp_group=None, xt=None, box=None):
     """linear(swiglu(linear(x, w_gu)), w_d): the Llama MLP (w_gu = [gate | up] on the output dimension).
     ``tp_group``: w_gu / w_d are the FFN-column / FFN-row shards of a tensor-parallel MLP; the input gradient
-    is summed over the group, overlapped with the gate|up weight gradient (the output sum is the caller's)."""
+    is summed over the group, overlapped with the gate|up weight gradient (the output sum is the caller's).
+    ``xt`` / ``box``: transposed operands from the neighbouring norms, as in ``linear``."""
     if not x.is_cuda:
         if tp_group is not None:
             from ..parallel.tensor import _CopyToTP
@@ -547,7 +680,7 @@ def swiglu_mlp(x, w_gu, w_d, tp_group=None):
             x = _CopyToTP.apply(x, tp_group)
         return F.linear(swiglu(F.linear(x, w_gu)), w_d)
     _gate(w_gu, w_d)
-    return _SwiGLUMLP.apply(x, w_gu, w_d, tp_group)
+    return _SwiGLUMLP.apply(x, w_gu, w_d, tp_group, xt, box)
 
 
 class _GELU(Function):
@@ -574,7 +707,7 @@ def gelu(x):
 # ---------------------------------------------------------------------------------------------------
 class _RopeAttention(Function):
     @staticmethod
-    def forward(ctx, qkv, cos, sin, B, S, Hq, Hkv, D, causal, scale, use_rope, inplace):
+    def forward(ctx, qkv, cos, sin, B, S, Hq, Hkv, D, causal, scale, use_rope, inplace, box=None, want_ot=False):
         lib = _lib()
         qkv = qkv.contiguous()
         if use_rope and not inplace:
@@ -587,13 +720,20 @@ class _RopeAttention(Function):
         T = qkv.shape[0]
         o = torch.empty(T, Hq * D, dtype=qkv.dtype, device=qkv.device)
         lse = torch.empty(B * Hq * S, dtype=torch.float32, device=qkv.device)
-        lib.flash_attn_fwd(q, k, v, o, lse, B, S, Hq, Hkv, D, scale, causal)
+        if want_ot:
+            ot = torch.empty(Hq * D, T, dtype=qkv.dtype, device=qkv.device)
+            lib.flash_attn_fwd_t(q, k, v, o, ot, lse, B, S, Hq, Hkv, D, scale, causal)
+            ctx.mark_non_differentiable(ot)
+            ctx.set_materialize_grads(False)  # no zero-filled [Hq*D, T] "gradient" of o^T
+        else:
+            lib.flash_attn_fwd(q, k, v, o, lse, B, S, Hq, Hkv, D, scale, causal)
         ctx.save_for_backward(qkv, o, lse, cos, sin)
         ctx.cfg = (B, S, Hq, Hkv, D, causal, scale, use_rope)
-        return o
+        ctx.box = box
+        return (o, ot) if want_ot else o
 
     @staticmethod
-    def backward(ctx, do):
+    def backward(ctx, do, dot=None):
         lib = _lib()
         qkv, o, lse, cos, sin = ctx.saved_tensors
         B, S, Hq, Hkv, D, causal, scale, use_rope = ctx.cfg
@@ -603,24 +743,38 @@ class _RopeAttention(Function):
         a, c = Hq * D, (Hq + Hkv) * D
         lib.flash_attn_bwd(qkv[:, :a], qkv[:, a:c], qkv[:, c:], o, do, lse, dqkv[:, :a], dqkv[:, a:c], dqkv[:, c:], ws,
                            B, S, Hq, Hkv, D, scale, causal)
-        if use_rope:
+        T, C = dqkv.shape
+        if ctx.box is not None and D in (64, 128) and T % 64 == 0 and C % 128 == 0 and ((Hq + Hkv) * D) % 128 == 0:
+            # inverse RoPE fused with dQKV^T for the QKV projection's weight gradient (csrc/transpose.hip rope_t)
+            dqkvt = torch.empty(C, T, dtype=dqkv.dtype, device=dqkv.device)
+            lib.rope_t_(dqkv, cos, sin, S, Hq + Hkv if use_rope else 0, D, True, dqkvt)
+            ctx.box.put(dqkv, dqkvt)
+        elif use_rope:
             lib.rope_(dqkv, cos, sin, None, S, Hq + Hkv, D, True)
-        return dqkv, None, None, None, None, None, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None, None, None, None, None, None, None
 
 
-def rope_attention(qkv, cos, sin, B, S, Hq, Hkv, D, causal=True, scale=None, use_rope=True, inplace=True):
+def rope_attention(qkv, cos, sin, B, S, Hq, Hkv, D, causal=True, scale=None, use_rope=True, inplace=True, box=None,
+                   want_ot=False):
     """Fused-QKV activation [B*S, (Hq+2Hkv)*D] -> attention output [B*S, Hq*D] (RoPE on Q,K if use_rope).
 
     With ``inplace`` (the model's setting) RoPE overwrites the Q/K columns of ``qkv`` -- safe there because
     the QKV projection's output has no other consumer -- saving one [T, (Hq+Hkv)D] copy per layer.
+    ``box`` (a ``TBox``): the backward also writes dQKV^T into it, for the QKV projection (``linear(box=)``).
+    ``want_ot``: return (o, o^T) -- o^T [Hq*D, B*S] from the forward kernel, the Wo projection's ``xt`` -- with
+    None in place of o^T where the kernel does not take the shape (S not a multiple of 256).
     """
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if not qkv.is_cuda:
         x = ref.rope_ref(qkv, cos, sin, S, Hq + Hkv, D) if use_rope else qkv
         a, c = Hq * D, (Hq + Hkv) * D
         o, _ = _attn_ref_autograd(x[:, :a], x[:, a:c], x[:, c:], B, S, Hq, Hkv, D, causal, scale)
-        return o
-    return _RopeAttention.apply(qkv, cos, sin, B, S, Hq, Hkv, D, causal, scale, use_rope, inplace)
+        return (o, None) if want_ot else o
+    ot = bool(want_ot) and S % 256 == 0 and D in (64, 128) and os.environ.get("KOP_FWD_VARIANT", "10") in ("8", "9", "10")
+    out = _RopeAttention.apply(qkv, cos, sin, B, S, Hq, Hkv, D, causal, scale, use_rope, inplace, box, ot)
+    if want_ot and not ot:
+        return out, None
+    return out
 
 
 def _attn_ref_autograd(q, k, v, B, S, Hq, Hkv, D, causal, scale):

@@ -18,7 +18,7 @@ SHAPES = {
     "gpt2": [(32768, 2304, 768, "qkv"), (32768, 768, 768, "proj"), (32768, 3072, 768, "fc"), (32768, 768, 3072, "out"),
              (32768, 50304, 768, "lm_head")],
     "llama": [(8192, 6144, 4096, "wqkv"), (8192, 4096, 4096, "wo"), (8192, 28672, 4096, "w_gate_up"),
-              (8192, 4096, 14336, "w_down")],
+              (8192, 4096, 14336, "w_down"), (8192, 128256, 4096, "lm_head")],
 }
 
 

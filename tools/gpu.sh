@@ -6,7 +6,7 @@
 #
 #   check        GPU test suite, smoke(), Llama-3-8B and GPT-2-small benches (what the driver runs at round end)
 #   tests        the GPU test suite only (SEL=<pytest selection> narrows it)
-#   bench        Llama-3-8B bench (ARGSETS="--a;--b" runs several argument sets back to back: same-box A/B)
+#   bench        Llama-3-8B bench (ARGSETS="--a;ENV=1 --b" runs several env / argument sets back to back: same-box A/B)
 #   gpt2         GPT-2-small bench (ARGSETS as above)
 #   prof-l8b     rocprofv3 kernel trace + stats of the Llama-3-8B step
 #   prof-gpt2    rocprofv3 kernel trace + stats of the GPT-2-small step
@@ -33,13 +33,18 @@ torchrun_n() {  # name limit nproc args...
     --master-port $port "$@"
 }
 
-argsets() {  # tag base-command: one bench per ';'-separated ARGSETS entry (default: the base command once)
-  local tag=$1 base=$2 i=0 a rc
+argsets() {  # tag base-command: one bench per ';'-separated ARGSETS entry (default: the base command once);
+  # an entry's leading NAME=value words are environment settings, the rest bench arguments
+  local tag=$1 base=$2 i=0 a tok
   IFS=';' read -ra SETS <<< "${ARGSETS:-}"
   [ ${#SETS[@]} -eq 0 ] && SETS=("")
   for a in "${SETS[@]}"; do
     i=$((i + 1))
-    step "${tag}_$i" 400 $base $a || return $?
+    local envs=() args=()
+    for tok in $a; do
+      if [ ${#args[@]} -eq 0 ] && [[ $tok == *=* && $tok != -* ]]; then envs+=("$tok"); else args+=("$tok"); fi
+    done
+    step "${tag}_$i" 400 env "${envs[@]}" $base "${args[@]}" || return $?
     grep -h '"metric"' "gpurun_out/${tag}_$i.log" | sed "s|^|[$a] |" | tee -a "gpurun_out/$tag.jsonl"
   done
 }

@@ -90,7 +90,9 @@ function formModal(title, fields, onSubmit, initial = {}) {
       else if (type === "checkbox") out[name] = el.checked;
       else out[name] = el.value;
     }
-    try { await onSubmit(out); closeModal(); route(); } catch (err) { $("#mf-err").textContent = err.message; }
+    // a submit that navigates (an operation opening its deploy tab) is rendered by the hashchange alone: a second
+    // route() here would render the same view twice, concurrently
+    try { const h = location.hash; await onSubmit(out); closeModal(); if (location.hash === h) route(); } catch (err) { $("#mf-err").textContent = err.message; }
   });
 }
 async function confirmDo(text, fn) { if (confirm(text)) { try { await fn(); route(); } catch (e) { alert(e.message); } } }
@@ -274,7 +276,7 @@ views.cluster = async (v, [name, tab = "overview", arg]) => {
     t.innerHTML = `<div class="row"><div style="flex:0 0 320px">${table(execs, [["Operation", (e) => `<a href="#/cluster/${esc(name)}/deploy/${esc(e.id)}">${esc(e.operation)}</a>`],
       ["State", (e) => st(e.state)], ["Time", (e) => `${(e.timedelta || 0).toFixed(1)}s`]])}</div>
       <div><div id="steps" class="steps"></div><pre class="term" id="term"></pre><div id="trace"></div></div></div>`;
-    if (cur) follow(cur, name);
+    if (cur) follow(cur, name, t);
   } else if (tab === "health") {
     const [h, hist, comps, nss] = await Promise.all([GET(`/cluster/${name}/health/all/`).catch((e) => ({error: e.message})), GET(`/clusterHealthHistory/${c.project_id}/`).catch(() => []),
       GET(`/cluster/${name}/component/`).catch(() => []), GET(`/cluster/${name}/namespace/`).catch(() => [])]);
@@ -389,9 +391,11 @@ async function showTrace(name, eid) {
   };
 }
 
-function follow(eid, name) {
+function follow(eid, name, root) {
+  // a render that lost the race to a newer one (its tab is no longer in the page) opens no sockets
+  if (root && $("#tab") !== root) return;
   closeSockets();
-  const term = $("#term"), steps = $("#steps");
+  const term = (root || document).querySelector("#term"), steps = (root || document).querySelector("#steps");
   const tok = localStorage.getItem("kop_token");
   const p = new WebSocket(wsURL(`/ws/progress/${eid}/?token=${encodeURIComponent(tok)}`));
   p.onmessage = (m) => { const d = JSON.parse(m.data); steps.innerHTML = (d.steps || []).map((s) => `<span class="${esc(s.status)}">${esc(s.name)}</span>`).join("") + ` ${st(d.state)}`;

@@ -1,7 +1,8 @@
 """The web UI's main flows, executed: tests/ui/flows.js runs the served index.html + app.js under node 12 over a
 small DOM (tests/ui/dom.js) against a live control plane (own ASGI server + job workers) on the simulated farm --
 sign in, cluster-create wizard with device checks, create & install followed over the progress / log websockets,
-and a PyTorch-ROCm training-chart deploy from the apps tab."""
+a PyTorch-ROCm training-chart deploy from the apps tab, then Day 2 through the forms: host registration, add-worker,
+backup storage + backup, LDAP settings, a new user, and the task monitor."""
 import asyncio
 import json
 import os
@@ -44,7 +45,7 @@ def test_ui_flows_against_a_live_control_plane(control):
     assert ready.wait(10)
     try:
         r = subprocess.run([NODE, "--harmony-nullish", "--harmony-optional-chaining", os.path.join(HERE, "ui", "flows.js"),
-                            f"http://127.0.0.1:{srv.port}", control.cfg["ADMIN_PASSWORD"]],
+                            f"http://127.0.0.1:{srv.port}", control.cfg["ADMIN_PASSWORD"], str(control.tmp / "bk")],
                            capture_output=True, text=True, timeout=240)
     finally:
         asyncio.run_coroutine_threadsafe(srv.stop(), loop).result(10)
@@ -62,4 +63,7 @@ def test_ui_flows_against_a_live_control_plane(control):
     assert all(s[1] == "success" for s in inst["steps"][:5]) and not inst["socket_errors"]
     assert inst["log_bytes"] > 1000
     assert "llama-train" in by["app-deployed"]["row"] and "tokens/s" in by["app-deployed"]["row"]
-    assert by["task-monitor"]["recent_jobs"] >= 2  # the install and the app deploy
+    assert "10.0.0.9" in by["host-registered"]["row"]
+    assert by["worker-added"]["nodes"] == 3 and "10.0.0.9" in by["worker-added"]["row"]
+    assert by["backup-done"]["backups"] == 1 and os.listdir(control.tmp / "bk" / "uiflow")
+    assert by["task-monitor"]["recent_jobs"] >= 4  # install, app deploy, add-worker, backup

@@ -4,8 +4,10 @@
 //   sign in -> cluster-create wizard with device / node-count checks against the template's requires
 //   (reference cluster-create.component.ts:394-505) -> create & install -> deploy tab following the progress and
 //   log websockets (reference deploy/component/term/term.component.ts:54-59) until SUCCESS, with the time
-//   breakdown -> apps tab: deploy the PyTorch-ROCm training chart and see its tokens/s result.
-// Usage: node --harmony-nullish --harmony-optional-chaining tests/ui/flows.js http://127.0.0.1:PORT PASSWORD
+//   breakdown -> apps tab: deploy the PyTorch-ROCm training chart and see its tokens/s result -> Day 2: register a
+//   host through its form, add it as a worker, create a backup storage and back the cluster up, save LDAP settings,
+//   add a user -> task monitor.
+// Usage: node --harmony-nullish --harmony-optional-chaining tests/ui/flows.js http://127.0.0.1:PORT PASSWORD [BACKUP_DIR]
 "use strict";
 const http = require("http");
 const crypto = require("crypto");
@@ -14,6 +16,7 @@ const {makeWindow, Event} = require("./dom");
 
 const BASE = process.argv[2];
 const PASSWORD = process.argv[3];
+const BACKUP_DIR = process.argv[4] || "/tmp/kop-ui-backups";
 const HOST = BASE.replace(/^http:\/\//, "");
 const log = (step, extra) => console.log(JSON.stringify(Object.assign({step}, extra || {})));
 
@@ -193,6 +196,66 @@ async function main() {
   const row = await until(() => doc.querySelectorAll("#tab table tr").find((r) => /llama-train/.test(r.textContent)), "release row");
   if (!/tokens\/s/.test(row.textContent)) throw new Error("no training result in the release row: " + row.textContent);
   log("app-deployed", {row: row.textContent.replace(/\s+/g, " ").trim()});
+  // ------------------------------------------------------------------ Day 2: register a host through its form,
+  // add it as a worker from the overview tab's operation buttons (reference cluster-status.component.ts:46-77)
+  const submitModal = (fill) => { const mf = $("#mf"); fill(mf.elements); mf.dispatchEvent(new Event("submit", {bubbles: true})); };
+  // an open form modal (a closed one keeps its old form in the DOM until the next one replaces it)
+  const openModal = (what) => until(() => !$("#modal").classList.contains("hidden") && $("#mf"), what);
+  const rowWith = (re) => doc.querySelectorAll("#view table tr").find((r) => re.test(r.textContent));
+  const runOp = async (op, fill, label) => {
+    win.location.hash = "#/cluster/uiflow/overview";
+    const btn = await until(() => doc.querySelector(`[data-op="${op}"]`), `${op} button`);
+    const before = win.location.hash;
+    btn.click();
+    await openModal(`${op} form`);
+    submitModal(fill);
+    await until(() => win.location.hash !== before && /^#\/cluster\/uiflow\/deploy\/.+/.test(win.location.hash), `${op} execution`);
+    const eid = win.location.hash.split("/").pop();
+    await until(() => rowWith(new RegExp(op)) && /SUCCESS/.test($("#steps").textContent), `${label} SUCCESS`, 90000);
+    return eid;
+  };
+  win.location.hash = "#/hosts";
+  await until(() => $("#add") && /Register host/.test($("#view").textContent), "hosts view");
+  $("#add").click();
+  await openModal("host form");
+  submitModal((el) => { el.name.value = "w2"; el.ip.value = "10.0.0.9"; el.password.value = "pw"; });
+  await until(() => rowWith(/w2.*10\.0\.0\.9/), "registered host row", 30000);
+  log("host-registered", {row: rowWith(/w2/).textContent.replace(/\s+/g, " ").trim()});
+  await runOp("add-worker", (el) => { el.host.value = "w2"; }, "add-worker");
+  win.location.hash = "#/cluster/uiflow/nodes";
+  const nodeRow = await until(() => rowWith(/10\.0\.0\.9/), "new worker in the nodes tab");
+  log("worker-added", {nodes: doc.querySelectorAll("#tab table tr").length - 1, row: nodeRow.textContent.replace(/\s+/g, " ").trim()});
+
+  // ------------------------------------------------------------------ backup storage (settings) -> backup operation
+  win.location.hash = "#/settings/backup-storage";
+  await until(() => $("#add") && /Backup storage/.test($("#view").textContent), "backup-storage tab");
+  $("#add").click();
+  await openModal("backup storage form");
+  submitModal((el) => { el.name.value = "ui-local"; el.type.value = "LOCAL"; el.credentials.value = JSON.stringify({path: BACKUP_DIR}); });
+  await until(() => rowWith(/ui-local/), "backup storage row");
+  await runOp("backup", () => {}, "backup");
+  win.location.hash = "#/cluster/uiflow/backup";
+  await until(() => $("#strat") && doc.querySelectorAll("#tab table tr").length >= 2, "backup listed in the backup tab");
+  log("backup-done", {backups: doc.querySelectorAll("#tab table").slice(-1)[0].querySelectorAll("tr").length - 1});
+
+  // ------------------------------------------------------------------ settings (LDAP tab) and a user
+  win.location.hash = "#/settings/ldap";
+  const sf = await until(() => $("#sf"), "ldap settings form");
+  sf.elements.AUTH_LDAP_SERVER_URI.value = "ldap://ldap.example.org:389";
+  sf.dispatchEvent(new Event("submit", {bubbles: true}));
+  await until(() => $("#sf-msg").textContent === "saved", "ldap settings saved");
+  win.location.hash = "#/settings/system";
+  await until(() => $("#sf") && $("#sf").elements.ntp_server, "system tab");
+  win.location.hash = "#/settings/ldap";
+  await until(() => $("#sf") && $("#sf").elements.AUTH_LDAP_SERVER_URI && $("#sf").elements.AUTH_LDAP_SERVER_URI.value === "ldap://ldap.example.org:389", "ldap setting read back");
+  win.location.hash = "#/users";
+  await until(() => $("#add") && /Users/.test($("#view").textContent), "users view");
+  $("#add").click();
+  await openModal("user form");
+  submitModal((el) => { el.username.value = "alice"; el.email.value = "alice@example.org"; el.password.value = "Secret-123"; });
+  await until(() => rowWith(/alice/), "user row");
+  log("settings-and-user", {ldap: "ldap://ldap.example.org:389"});
+
   // ------------------------------------------------------------------ task monitor (the reference's Flower)
   win.location.hash = "#/tasks";
   await until(() => /Task monitor/.test($("#view").textContent) && /online/.test($("#view").textContent), "task monitor with an online worker");

@@ -609,6 +609,16 @@ def create_app() -> FastAPI:
             h = dict(h, pods=[p for p in _cached(c.name)["pods"] if p["namespace"] == ns])
         return h
 
+    @r.post("/cluster/{name}/monitor/refresh/")
+    def cluster_monitor_refresh(name: str, request: Request):
+        """Collect the cluster's dashboard data now instead of at the next 5-minute tick (UI dashboard refresh)."""
+        c = _cluster_for(current_user(request), name)
+        try:
+            d = monitor.set_cluster_data(c.name)
+        except Exception as e:  # noqa: BLE001 -- cluster API unreachable: the cached blob stays
+            raise HTTPError(502, f"monitoring data of {c.name} not refreshed: {e}") from e
+        return {"name": c.name, "date": d["date"]}
+
     @r.get("/cluster/{name}/component/")
     def cluster_components(name: str, request: Request):
         c = _cluster_for(current_user(request), name)

@@ -118,18 +118,46 @@ function crudPage(title, path, cols, fields, opts = {}) {
 // ------------------------------------------------------------------ views
 const views = {};
 
-views.dashboard = async (v) => {
-  const [clusters, hosts, dash] = await Promise.all([GET("/clusters/"), GET("/host/"), GET("/dashboard/all/all/").catch(() => ({}))]);
+// dashboard (reference dashboard.component.html): item / cluster filters, cluster status, capacity (CPU, memory,
+// AMD GPUs), statistics (nodes, pods, namespaces, deployments), warnings, restarting and failing pods. The monitor
+// collects every 5 minutes (domain/monitor.py); "refresh" re-reads it.
+views.dashboard = async (v, [item = "all", cluster = "all"]) => {
+  const [clusters, hosts, items] = await Promise.all([GET("/clusters/"), GET("/host/"), GET("/items/").catch(() => [])]);
+  const dash = await GET(`/dashboard/${encodeURIComponent(cluster)}/${encodeURIComponent(item)}/`).catch(() => ({clusters: []}));
   const gpus = hosts.reduce((a, h) => a + (h.gpu_num || 0), 0);
   const running = clusters.filter((c) => c.status === "RUNNING").length;
-  v.innerHTML = `<h2>Dashboard</h2><div class="grid">
+  const data = dash.clusters || [];
+  const sum = (k) => data.reduce((a, d) => a + ((d[k] || []).length || 0), 0);
+  const pct = (x) => `${Math.round(100 * (x || 0))} %`;
+  const shown = item === "all" ? clusters : clusters.filter((c) => c.item_name === item);
+  v.innerHTML = `<h2>Dashboard</h2><div class="toolbar"><select id="d-item" style="width:auto"><option value="all">all items</option>
+      ${items.map((i) => `<option ${i.name === item ? "selected" : ""}>${esc(i.name)}</option>`).join("")}</select>
+    <select id="d-cluster" style="width:auto"><option value="all">all clusters</option>${shown.map((c) => `<option ${c.name === cluster ? "selected" : ""}>${esc(c.name)}</option>`).join("")}</select>
+    <button id="d-refresh" class="secondary">refresh</button><span class="muted">monitoring data every 5 minutes</span></div>
+    <div class="grid">
     <div class="card stat"><div class="v">${clusters.length}</div><div class="k">clusters (${running} running)</div></div>
     <div class="card stat"><div class="v">${hosts.length}</div><div class="k">hosts</div></div>
     <div class="card stat"><div class="v">${gpus}</div><div class="k">AMD Instinct GPUs registered</div></div>
     <div class="card stat"><div class="v">${dash.gpu_allocatable ?? 0}/${dash.gpu_total ?? 0}</div><div class="k">amd.com/gpu allocatable / capacity</div></div>
-    </div><h3>Clusters</h3>${table(clusters, [["Name", (c) => `<a href="#/cluster/${esc(c.name)}">${esc(c.name)}</a>`], ["Status", (c) => st(c.status)],
+    </div><h3>Cluster status</h3>${table(shown, [["Name", (c) => `<a href="#/cluster/${esc(c.name)}">${esc(c.name)}</a>`], ["Status", (c) => st(c.status)],
       ["Template", "template"], ["Nodes", "node_size"], ["GPUs", "gpu_num"], ["Package", "package"]])}
-    <h3>Pods restarting / failing</h3>${table([...(dash.restart_pods || []), ...(dash.error_pods || [])], [["Namespace", "namespace"], ["Pod", "name"], ["Status", "status"], ["Restarts", "restart_count"]], "All pods healthy (or no monitoring data yet).")}`;
+    <h3>Capacity</h3>${table(data, [["Cluster", "name"], ["CPU used", (d) => pct(d.cpu_usage)], ["Memory used", (d) => pct(d.mem_usage)],
+      ["amd.com/gpu", (d) => `${esc(d.gpu_allocatable ?? 0)} / ${esc(d.gpu_total ?? 0)}`], ["Collected", "date"]], "No monitoring data yet.")}
+    <h3>Statistics</h3><div class="grid">
+      <div class="card stat"><div class="v">${sum("nodes")}</div><div class="k">nodes</div></div>
+      <div class="card stat"><div class="v">${sum("pods")}</div><div class="k">pods</div></div>
+      <div class="card stat"><div class="v">${sum("namespaces")}</div><div class="k">namespaces</div></div>
+      <div class="card stat"><div class="v">${sum("deployments")}</div><div class="k">deployments</div></div></div>
+    <h3>Warnings</h3>${table(dash.warn_containers || [], [["Cluster / node", (w) => esc(w.cluster || w.node || w.name || "")], ["Check", (w) => esc(w.type || w.reason || "")],
+      ["Detail", (w) => esc(w.message || JSON.stringify(w))]], "No warnings.")}
+    <h3>Pods restarting</h3>${table(dash.restart_pods || [], [["Namespace", "namespace"], ["Pod", "name"], ["Status", "status"], ["Restarts", "restart_count"]], "None.")}
+    <h3>Pods failing</h3>${table(dash.error_pods || [], [["Namespace", "namespace"], ["Pod", "name"], ["Status", "status"], ["Restarts", "restart_count"]], "All pods healthy (or no monitoring data yet).")}`;
+  $("#d-item").onchange = (e) => { location.hash = `#/dashboard/${encodeURIComponent(e.target.value)}/all`; };
+  $("#d-cluster").onchange = (e) => { location.hash = `#/dashboard/${encodeURIComponent(item)}/${encodeURIComponent(e.target.value)}`; };
+  $("#d-refresh").onclick = async () => {
+    for (const c of cluster === "all" ? shown : shown.filter((x) => x.name === cluster)) await POST(`/cluster/${c.name}/monitor/refresh/`).catch(() => null);
+    route();
+  };
 };
 
 views.clusters = async (v) => {

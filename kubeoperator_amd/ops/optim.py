@@ -16,9 +16,16 @@ runs underneath the next step's compute-bound forward instead of in its own seri
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
+
+# race-detection hook: GPU clock cycles of ``torch.cuda._sleep`` enqueued on the optimizer stream before every
+# bucket's update, so the stream deterministically lags the compute stream; a forward that read a bucket without
+# waiting for its gate, or a backward that overwrote gradients AdamW still reads, then changes the result
+# (tests/test_stream_lag_gpu.py; ops.functional.SIDE_LAG_CYCLES is the weight-gradient stream's twin)
+OPTIM_LAG_CYCLES = int(os.environ.get("KOP_OPTIM_LAG_CYCLES", "0"))
 
 
 @dataclass
@@ -141,6 +148,8 @@ class FusedAdamW:
             self._stream.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(self._stream):
                 for k in self._launch_order():
+                    if OPTIM_LAG_CYCLES > 0:
+                        torch.cuda._sleep(OPTIM_LAG_CYCLES)
                     launch(k)
                     b = self.segments[k].bucket
                     gate = self.on_segment(self.segments[k]) if self.on_segment is not None else None

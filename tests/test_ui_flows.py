@@ -66,4 +66,5 @@ def test_ui_flows_against_a_live_control_plane(control):
     assert "10.0.0.9" in by["host-registered"]["row"]
     assert by["worker-added"]["nodes"] == 3 and "10.0.0.9" in by["worker-added"]["row"]
     assert by["backup-done"]["backups"] == 1 and os.listdir(control.tmp / "bk" / "uiflow")
+    assert {"Cluster status", "Capacity", "Statistics", "Pods failing"} <= set(by["dashboard"]["cards"])
     assert by["task-monitor"]["recent_jobs"] >= 4  # install, app deploy, add-worker, backup

@@ -256,6 +256,17 @@ async function main() {
   await until(() => rowWith(/alice/), "user row");
   log("settings-and-user", {ldap: "ldap://ldap.example.org:389"});
 
+  // ------------------------------------------------------------------ dashboard filters (item -> cluster list)
+  win.location.hash = "#/dashboard";
+  await until(() => $("#d-item") && /Cluster status/.test($("#view").textContent), "dashboard cards");
+  const itemSel = $("#d-item");
+  itemSel.value = itemSel.options[1].value;  // the seeded default item
+  itemSel.dispatchEvent(new Event("change"));
+  await until(() => /^#\/dashboard\/[^/]+\/all$/.test(win.location.hash) && rowWith(/uiflow/), "cluster under its item");
+  $("#d-refresh").click();  // no Kubernetes API on the simulated farm: the refresh fails quietly, the view re-renders
+  await until(() => $("#d-item") && /Statistics/.test($("#view").textContent), "dashboard after refresh");
+  log("dashboard", {cards: doc.querySelectorAll("#view h3").map((h) => h.textContent)});
+
   // ------------------------------------------------------------------ task monitor (the reference's Flower)
   win.location.hash = "#/tasks";
   await until(() => /Task monitor/.test($("#view").textContent) && /online/.test($("#view").textContent), "task monitor with an online worker");

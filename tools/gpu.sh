@@ -14,7 +14,7 @@
 #   attn-probe   attention TF/s per shape; VARIANTS="ENV=a;ENV=b;base" alternates env variants twice
 #   dp           one-GPU data-parallel rehearsals (2 / 4 gloo ranks sharing cuda:0) + bench.py --gpus 2 under torchrun
 #   tp           one-GPU tensor (+ sequence) parallel rehearsals + bench.py --tp 2 [--sp 1] + 4 Llama-3-70B layers
-#   wgrad-lag    weight-gradient side stream under a forced lag: GPU tests, then DP / TP rehearsals with it on
+#   wgrad-lag    weight-gradient and optimizer streams under a forced lag: GPU tests, then DP / TP rehearsals
 #   wgrad-splitk weight-gradient GEMM forms at the training shapes (tools/bench_wgrad_splitk.py)
 #   tune         TunableOp tuning of the training GEMMs, then heuristic vs tuned bench
 #   tune-decode  TunableOp tuning of the decode GEMMs, then the decode benchmark
@@ -119,8 +119,9 @@ s_tp() {
 }
 
 s_wgrad_lag() {
-  step wgrad_tests 600 python -u -m pytest tests/test_wgrad_stream_gpu.py -x -v --timeout 200 --timeout-method thread && (
-    export KOP_WGRAD_STREAM=1 KOP_SIDE_LAG_CYCLES=200000
+  step wgrad_tests 600 python -u -m pytest tests/test_wgrad_stream_gpu.py tests/test_stream_lag_gpu.py -x -v --timeout 200 \
+    --timeout-method thread && (
+    export KOP_WGRAD_STREAM=1 KOP_SIDE_LAG_CYCLES=200000 KOP_OPTIM_LAG_CYCLES=200000
     rehearse 2 tools/dp_rehearsal.py --mode zero1 && \
     rehearse 4 tools/dp_rehearsal.py --mode zero1 --accum 4 && \
     rehearse 4 tools/dp_rehearsal.py --mode allreduce && \

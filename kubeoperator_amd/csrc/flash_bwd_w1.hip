@@ -1,0 +1,484 @@
+// Flash attention BACKWARD, dK / dV stage with one wave per SIMD (gfx950 / MI355X), D = 128.
+// Built with -mllvm -amdgpu-mfma-vgpr-form=true (ops/_build.py FILE_FLAGS): the S / dP MFMAs are VGPR-form
+// builtins (their results feed the softmax VALU directly, hipcc pads those hazards), while the dK^T / dV^T
+// chains are inline-asm MFMAs on "+a" operands -- 256 accumulators pinned in the AGPR half of the 512-register
+// file. (Left to its heuristic, hipcc put every MFMA in AGPR form: 320 AGPRs of demand for 256, ~600
+// v_accvgpr moves per stage.) Wait states the asm needs: 2 after a VALU write of an A / B operand (the s_nop 1
+// opening each statement); 18 after the last MFMA before the accumulators are read (the epilogue nop statement).
+#include "attn_common.h"
+#include "kernels.h"
+
+namespace kop {
+
+// 16-byte LDS read (4 floats) at a lane base + immediate, retired by the caller's counted lgkmcnt
+template <int OFF>
+__device__ __forceinline__ f32x4 lds_read16f_off(uint32_t base) {
+  f32x4 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(base), "n"(OFF));
+  return r;
+}
+__device__ __forceinline__ f32x16 cat4f(const f32x4* q) {
+  return f32x16{q[0][0], q[0][1], q[0][2], q[0][3], q[1][0], q[1][1], q[1][2], q[1][3],
+                q[2][0], q[2][1], q[2][2], q[2][3], q[3][0], q[3][1], q[3][2], q[3][3]};
+}
+
+// QM staging write: lane r holds key r (of the block at byte offset BLK), queries 16S + {0-3, 8-11} (+4 for hh = 1);
+// one permlane32_swap per dword pairs the halves into queries 16S + 8hh .. +7 (16 B) -> one ds_write_b128
+template <int S16, int BLK>
+__device__ __forceinline__ void stage_w(const u32x4& w, uint32_t base, std::integral_constant<int, BLK>) {
+  const auto a = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
+  const auto c = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
+  const u32x4 o = {a[0], c[0], a[1], c[1]};
+  asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(base), "v"(o), "n"(BLK));
+}
+// QM store instruction I: 8 slot-ordered keys (two transposed reads) of one query row -> 16 B
+template <int I, bool NT = false>
+__device__ __forceinline__ void stage_st(const bf16x4* x, uint64_t base, uint32_t off) {
+  const u32x4 o = __builtin_bit_cast(u32x4, cat44(x[0], x[1]));
+  if constexpr (NT)
+    asm volatile("global_store_dwordx4 %0, %1, %2 offset:%3 nt\n\ts_nop 1" ::"v"(off), "v"(o), "s"(base), "n"(32 * I)
+                 : "memory");
+  else
+    asm volatile("global_store_dwordx4 %0, %1, %2 offset:%3\n\ts_nop 1" ::"v"(off), "v"(o), "s"(base), "n"(32 * I)
+                 : "memory");
+}
+
+// acc += a . b on the 32x32x16 bf16 MFMA with the accumulator in AGPRs (a dependent chain needs no wait states)
+__device__ __forceinline__ void mfma32_agpr(f32x16& acc, bf16x8 a, bf16x8 b) {
+  asm("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+
+// =============================================================================================
+// dK / dV, one wave per SIMD (KOP_DKDV_CFG 64, the default at D = 128)
+// =============================================================================================
+// The 2-waves-per-SIMD kernel (flash_bwd.hip fa_bwd_dkdv_kernel) gives each wave 32 keys, so every staged Q / dO tile is re-read from LDS
+// per 32 keys (40 KB of LDS reads per wave per 32 MFMAs: the LDS array, not the matrix pipe, paced it --
+// profiles/r3_attn_pmc_summary.txt) and it stored dS as 2-byte scatters (16 stores + 64 SALU address adds per
+// stage). Here one 256-thread workgroup holds a CU alone (__launch_bounds__(256, 1): 512 registers per wave)
+// and each wave owns 64 keys:
+//   * dK^T / dV^T for 64 keys x 128 columns are 256 fp32 accumulators: the AGPR half of the register file;
+//     V^T fragments of the 64 keys stay resident in VGPRs; every Q / dO fragment read from LDS feeds two
+//     MFMAs (48 KB of LDS reads per 64 MFMAs);
+//   * -lse / scale and -delta of the stage's 32 queries are the C operands of the first S and dP MFMAs
+//     (shared by both 32-key blocks: no accumulator-initialisation moves), so p = exp2(c * acc), dS = p * acc;
+//   * per stage: S (16 MFMAs) | dP (16) beside the exponentials | dV (16) beside dS | dK (16) -- each VALU
+//     phase has an independent MFMA phase to hide under;
+//   * dS is stored TRANSPOSED ([B, Hq, key, query], unscaled bf16): the accumulator holds one key per lane and
+//     4-query runs per register quad, so one v_permlane32_swap per dword pairs the two lane halves into
+//     8-query (16 B) runs -- 4 dwordx4 stores per wave per stage instead of 32 two-byte stores.
+// Stage ring: Q / dO / {-lse/scale, -delta} of 32 queries, NS deep, behind counted vmcnt + raw barriers.
+#define KOP_VM_CASE(n) \
+  case n:              \
+    asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); \
+    break;
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (0..15)
+__device__ __forceinline__ void vm_wait_le(int n) {
+  switch (n) {
+    KOP_VM_CASE(0) KOP_VM_CASE(1) KOP_VM_CASE(2) KOP_VM_CASE(3) KOP_VM_CASE(4) KOP_VM_CASE(5) KOP_VM_CASE(6)
+    KOP_VM_CASE(7) KOP_VM_CASE(8) KOP_VM_CASE(9) KOP_VM_CASE(10) KOP_VM_CASE(11) KOP_VM_CASE(12) KOP_VM_CASE(13)
+    KOP_VM_CASE(14)
+    default:
+      asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
+  }
+}
+#undef KOP_VM_CASE
+
+// DIAG (timing ablations, KOP_DKDV64_DIAG): 1 no dS stores, 2 no exponentials, 4 no stage DMA, 8 no stage barrier,
+// 32 no DMA wait (all of these give wrong results); 16 non-temporal dS stores (correct)
+// QM: dS in the query-major layout of fa_bwd_dkdv_kernel ([B, Hq, query, slot(key)]), staged through LDS so each
+// wave writes whole 128-B lines (its 64 keys are one line of every query row); else transposed, stored directly.
+template <int D, bool DIRECT, int NS, bool QM, int DIAG = 0>
+__global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
+    const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
+    const bf16_t* __restrict__ dout, const float* __restrict__ nlse, const float* __restrict__ ndelta,
+    float* __restrict__ dk_part, float* __restrict__ dv_part, bf16_t* __restrict__ dst, int B, int S, int Hq, int Hkv,
+    int64_t qs, int64_t ks, int64_t vs, int64_t dos, float scale, int causal, int64_t dks, int64_t dvs) {
+  constexpr int NW = 4, KW = 64, BN = NW * KW, BQ = 32, ROWB = D * 2;
+  constexpr int KB = BN * ROWB, QT = BQ * ROWB, STAGE = 2 * QT + 1024;
+  constexpr int MYP = (2 * QT / 1024) / NW;  // Q / dO DMA pieces per wave per stage
+  static_assert(MYP * NW * 1024 == 2 * QT, "stage must split evenly over the waves");
+  constexpr int DT = D / 32, NK = D / 16, RB = ROWB * 8;
+  static_assert(NS == 3, "the vmcnt bookkeeping below tracks the stores of the two previous stages");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const Kl = smem;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hh = lane >> 5;
+  const int tq = (lane & 15) >> 2, tp = lane & 3, tg1 = (lane >> 4) & 1;
+  const int nkb = S / BN;
+  const AttnWork aw = attn_work(blockIdx.x, B, Hq, Hq / Hkv, nkb);
+  const int kb = aw.rank;  // heaviest key blocks (earliest keys under a causal mask) first
+  const int b = aw.b, hq = aw.unit;
+  const int kvh = hq / (Hq / Hkv);
+  const int k0 = kb * BN, k0w = k0 + KW * wid;
+  const float c2 = scale * 1.4426950408889634f;
+
+  const float* lse_h = nlse + ((int64_t)(b * Hq + hq)) * S;
+  const float* del_h = ndelta + ((int64_t)(b * Hq + hq)) * S;
+  const bf16_t* qbase = q + (int64_t)(b * S) * qs + hq * D;
+  const bf16_t* dobase = dout + (int64_t)(b * S) * dos + hq * D;
+  const int qt0 = causal ? k0 / BQ : 0;
+  const int nqt = S / BQ;
+
+  auto issue = [&](int qt) {
+    char* base = smem + KB + ((qt - qt0) % NS) * STAGE;
+    const int q0 = qt * BQ;
+    dma_tile_a<ROWB, NW, BQ>(base, qbase + (int64_t)q0 * qs, qs, wid, lane);
+    dma_tile_a<ROWB, NW, BQ>(base + QT, dobase + (int64_t)q0 * dos, dos, wid, lane);
+    if (wid == 0) {
+      const int l = lane & 15;
+      const float* src = (l < 8 ? lse_h + q0 + 4 * l : del_h + q0 + 4 * (l - 8));
+      glds16(src, base + 2 * QT);
+    }
+  };
+  dma_tile_a<ROWB, NW, BN>(Kl, k + (int64_t)(b * S + k0) * ks + kvh * D, ks, wid, lane);
+  issue(qt0);
+#pragma unroll
+  for (int i = 1; i < NS - 1; ++i)
+    if (qt0 + i < nqt) issue(qt0 + i);
+
+  const int rb_lane0 = RB * (r >> 3) + 64 * (r & 7) + 16 * (hh ^ ((r >> 2) & 3));
+  const int rb_lane1 = RB * (r >> 3) + 64 * (r & 7) + 16 * ((2 + hh) ^ ((r >> 2) & 3));
+  const int tb_lane0 = 64 * (4 * hh + tq) + 16 * ((2 * tg1 + (tp >> 1)) ^ hh) + 8 * (tp & 1);
+  const int tb_lane1 = 64 * (4 * hh + tq) + 16 * ((2 * tg1 + (tp >> 1)) ^ (2 + hh)) + 8 * (tp & 1);
+
+  // V^T fragments of the wave's 64 keys (B operand of dP = dO.V^T; key = k0w + 32*c + r), resident
+  bf16x8 vf0[NK], vf1[NK];
+  {
+    const bf16_t* vp = v + (int64_t)(b * S + k0w + r) * vs + kvh * D + 8 * hh;
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      vf0[kk] = *reinterpret_cast<const bf16x8*>(vp + 16 * kk);
+      vf1[kk] = *reinterpret_cast<const bf16x8*>(vp + 32 * vs + 16 * kk);
+    }
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) asm volatile("" : "+v"(vf0[kk]), "+v"(vf1[kk]));
+  }
+  f32x16 dk0[DT], dk1[DT], dv0[DT], dv1[DT];
+#pragma unroll
+  for (int i = 0; i < DT; ++i) dk0[i] = dk1[i] = dv0[i] = dv1[i] = f32x16{0};
+
+  const int pcount = MYP + (wid == 0 ? 1 : 0);  // DMA ops this wave issues per stage
+  int st1 = 0, st2 = 0;                           // dS stores issued in the previous / second-previous stage
+  // dS^T rows of the wave's keys: row pointer in SGPRs, lane offset (key r, queries 16s + 8hh) in one VGPR
+  const uint64_t dsrow = (uint64_t)(uintptr_t)(dst + ((int64_t)(b * Hq + hq) * S + k0w) * S);
+  const uint32_t dsoff = 2u * (uint32_t)(r * S + 8 * hh);
+  // QM staging image of the wave's stage tile: [64 keys][32 queries] bf16, 64-B rows, 16-B chunks XOR-swizzled
+  // by (key >> 1) & 3. Writes: lane (key r of block c, queries 16s + 8hh ..) -> chunk 2s + hh. Transposed reads:
+  // lane group G = lane >> 4 reads keys 16i + 4(G >> 1) + {0-3} and +8 (slot order) for queries 16(G & 1) + (lane & 15)
+  // in store instruction i; the store puts those 8 keys (16 B) at dS[query][k0w + 16i + 8(G >> 1)].
+  char* const stg = smem + KB + NS * STAGE + wid * 4096;
+  const int xw = (r >> 1) & 3;
+  const uint32_t stw0 = lds_addr(stg) + 64 * r + 16 * (hh ^ xw), stw1 = lds_addr(stg) + 64 * r + 16 * ((2 + hh) ^ xw);
+  const int sg = lane >> 4, si = lane & 15, sq = si >> 2, sp = si & 3;
+  const int skey = 4 * (sg >> 1) + sq;
+  const uint32_t str = lds_addr(stg) + 64 * skey + 16 * ((2 * (sg & 1) + (sp >> 1)) ^ ((skey >> 1) & 3)) + 8 * (sp & 1);
+  const uint64_t dsq = (uint64_t)(uintptr_t)(dst + ((int64_t)(b * Hq + hq) * S) * S + k0w);
+  const uint32_t sqoff = 2u * (uint32_t)((16 * (sg & 1) + si) * S + 8 * (sg >> 1));
+  (void)stw0; (void)stw1; (void)str; (void)dsq; (void)sqoff;
+
+  auto body = [&](int qt, auto mask_c) {
+    constexpr bool MASK = decltype(mask_c)::value;
+    // DMA(qt) is older than: stores(qt-2), DMA(qt+NS-2), stores(qt-1) (and the other DMAs still in flight)
+    int younger = st1 + st2;
+#pragma unroll
+    for (int i = 1; i < NS - 1; ++i) younger += (qt + i < nqt) ? pcount : 0;
+    if constexpr (!(DIAG & 36)) vm_wait_le(younger);
+    st2 = st1;
+    st1 = 0;
+    if constexpr (!(DIAG & 8)) __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if constexpr (!(DIAG & 4)) {
+      if (qt + NS - 1 < nqt) issue(qt + NS - 1);
+    }
+    const int qs0 = qt * BQ;
+    if (causal && qs0 + BQ - 1 < k0w) return;  // every query of the stage precedes every key of the wave
+    const char* Ql = smem + KB + ((qt - qt0) % NS) * STAGE;
+    const char* Ol = Ql + QT;
+    // Every LDS read below is an inline-asm read retired by a counted lgkmcnt, and every step ends in
+    // sched_barrier(0): left to itself hipcc sank the MFMAs below later reads, which serialised them (one wave
+    // per SIMD has no partner wave to hide that). Prefetch distance: 3 steps for row reads, 1 step (the 4 MFMAs
+    // of a step, 128 cycles) for transposed reads.
+    const uint32_t qb0 = lds_addr(Ql) + rb_lane0, qb1 = lds_addr(Ql) + rb_lane1;
+    const uint32_t ob0 = lds_addr(Ol) + rb_lane0, ob1 = lds_addr(Ol) + rb_lane1;
+    const uint32_t kw0 = lds_addr(Kl) + rb_lane0 + RB * 8 * wid, kw1 = lds_addr(Kl) + rb_lane1 + RB * 8 * wid;
+    const uint32_t o0 = lds_addr(Ol) + tb_lane0, o1 = lds_addr(Ol) + tb_lane1;
+    const uint32_t qa0 = lds_addr(Ql) + tb_lane0, qa1 = lds_addr(Ql) + tb_lane1;
+    // -lse/scale (bytes 0..127) and -delta (128..255) of the stage's queries; accumulator row j is query
+    // (j&3) + 8(j>>2) + 4hh, i.e. floats 8g + 4hh .. +3 for register quad g
+    const uint32_t ldb = lds_addr(Ql + 2 * QT) + 16 * hh;
+    auto grp = [&](auto kc, bf16x8* d3) {  // S-phase row reads of k-step kk: Q row, K rows of both key blocks
+      constexpr int kk = decltype(kc)::value;
+      d3[0] = lds_read8_off<512 * (kk >> 1)>((kk & 1) ? qb1 : qb0);
+      d3[1] = lds_read8_off<512 * (kk >> 1)>((kk & 1) ? kw1 : kw0);
+      d3[2] = lds_read8_off<RB * 4 + 512 * (kk >> 1)>((kk & 1) ? kw1 : kw0);
+    };
+    auto dor = [&](auto kc) {  // dP-phase row read of k-step kk: dO row
+      constexpr int kk = decltype(kc)::value;
+      return lds_read8_off<512 * (kk >> 1)>((kk & 1) ? ob1 : ob0);
+    };
+    auto trr = [&](uint32_t b0, uint32_t b1, auto dtc, bf16x4* t) {  // transposed reads of column block dt
+      constexpr int dt = decltype(dtc)::value;
+      t[0] = lds_tr_read_off<512 * dt>(b0);
+      t[1] = lds_tr_read_off<RB + 512 * dt>(b1);
+      t[2] = lds_tr_read_off<RB * 2 + 512 * dt>(b0);
+      t[3] = lds_tr_read_off<RB * 3 + 512 * dt>(b1);
+    };
+    using I = std::integral_constant<int, 0>;
+    (void)I{};
+    // ---- S = Q.K^T (16 MFMAs); the -lse/scale C operand is shared by both key blocks
+    f32x4 lq[4];
+    static_for<4>([&](auto g) { lq[decltype(g)::value] = lds_read16f_off<32 * decltype(g)::value>(ldb); });
+    bf16x8 ga[3], gb[3], gc[3];
+    grp(std::integral_constant<int, 0>{}, ga);
+    grp(std::integral_constant<int, 1>{}, gb);
+    grp(std::integral_constant<int, 2>{}, gc);
+    asm volatile("s_waitcnt lgkmcnt(9)" : "+v"(lq[0]), "+v"(lq[1]), "+v"(lq[2]), "+v"(lq[3]));
+    const f32x16 cl = cat4f(lq);
+    f32x16 s0, s1;
+    bf16x8 dof[3];
+    f32x4 ld[4];
+    static_for<NK>([&](auto kc) {
+      constexpr int kk = decltype(kc)::value;
+      bf16x8* cur = (kk % 3 == 0) ? ga : (kk % 3 == 1) ? gb : gc;
+      // younger than group kk: the next two groups, and from step NK-2 on the dP phase's 7 early reads
+      constexpr int younger = 3 * (NK - 1 - kk < 2 ? NK - 1 - kk : 2) + (kk > NK - 3 ? 7 : 0);
+      wait_rows3<younger>(cur);
+      s0 = mfma32(cur[0], cur[1], kk == 0 ? cl : s0);
+      s1 = mfma32(cur[0], cur[2], kk == 0 ? cl : s1);
+      if constexpr (kk + 3 < NK) grp(std::integral_constant<int, kk + 3>{}, cur);
+      if constexpr (kk == NK - 3) {  // the dP phase's first reads fly under the last S MFMAs
+        static_for<4>([&](auto g) { ld[decltype(g)::value] = lds_read16f_off<128 + 32 * decltype(g)::value>(ldb); });
+        static_for<3>([&](auto i) { dof[decltype(i)::value] = dor(i); });
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    // ---- dP = dO.V^T (16 MFMAs) beside p = exp2(c * acc) and its bf16 packing (2 score pairs per block per step)
+    const int kd = k0w + r - qs0 - 4 * hh;  // key - query + ((j&3) + 8(j>>2)) for register j of block 0
+    (void)kd;
+    f32x16 p0, p1;
+    u32x4 pw0[2], pw1[2];
+    bf16x4 ta[4], tb[4];
+    static_for<NK>([&](auto kc) {
+      constexpr int kk = decltype(kc)::value;
+      bf16x8& cur = dof[kk % 3];
+      // younger than dO row kk: the next two rows, and from step NK-2 on the dV phase's 4 early transposed reads
+      constexpr int younger = (NK - 1 - kk < 2 ? NK - 1 - kk : 2) + (kk > NK - 3 ? 4 : 0);
+      if constexpr (kk == 0) {
+        asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(ld[0]), "+v"(ld[1]), "+v"(ld[2]), "+v"(ld[3]) : "n"(younger + 1));
+        asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(cur) : "n"(younger));
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(cur) : "n"(younger));
+      }
+      if constexpr (kk == 0) {
+        const f32x16 cd = cat4f(ld);
+        p0 = mfma32(cur, vf0[kk], cd);
+        p1 = mfma32(cur, vf1[kk], cd);
+      } else {
+        p0 = mfma32(cur, vf0[kk], p0);
+        p1 = mfma32(cur, vf1[kk], p1);
+      }
+      if constexpr (kk + 3 < NK) cur = dor(std::integral_constant<int, kk + 3>{});
+      if constexpr (kk == NK - 3) trr(o0, o1, std::integral_constant<int, 0>{}, ta);
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        constexpr int j0 = 2 * kk;
+        const int j = j0 + e;
+        float a = (DIAG & 2) ? s0[j] * c2 : __builtin_amdgcn_exp2f(s0[j] * c2);
+        float c = (DIAG & 2) ? s1[j] * c2 : __builtin_amdgcn_exp2f(s1[j] * c2);
+        if constexpr (MASK) {
+          if (kd > (j & 3) + 8 * (j >> 2)) a = 0.f;
+          if (kd + 32 > (j & 3) + 8 * (j >> 2)) c = 0.f;
+        }
+        s0[j] = a;
+        s1[j] = c;
+      }
+      pw0[kk >> 2][kk & 3] = pack2(s0[2 * kk], s0[2 * kk + 1]);
+      pw1[kk >> 2][kk & 3] = pack2(s1[2 * kk], s1[2 * kk + 1]);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    const bf16x8 pb0[2] = {__builtin_bit_cast(bf16x8, pw0[0]), __builtin_bit_cast(bf16x8, pw0[1])};
+    const bf16x8 pb1[2] = {__builtin_bit_cast(bf16x8, pw1[0]), __builtin_bit_cast(bf16x8, pw1[1])};
+    // ---- dV^T += dO^T.P (16 MFMAs; each transposed fragment feeds both key blocks) beside dS = p * (dP - delta),
+    // its packing and the transposed dS stores
+    u32x4 sw0[2], sw1[2];
+    const uint64_t row0 = dsrow + 2ull * (uint64_t)qs0, row1 = row0 + 2ull * 32ull * (uint64_t)S;
+    auto st = [](const u32x4& w, uint64_t row, int s, uint32_t off) {
+      // lane r holds key r, queries 16s + {0-3, 8-11} (+4 for hh = 1); one permlane32_swap per dword pairs the
+      // halves into queries 16s + 8hh .. +7: 16 B per lane
+      const auto a = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
+      const auto c = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
+      const u32x4 o = {a[0], c[0], a[1], c[1]};
+      const uint64_t rs = row + 32ull * (uint64_t)s;
+      asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" ::"v"(off), "v"(o), "s"(rs) : "memory");
+    };
+    static_for<DT>([&](auto dtc) {
+      constexpr int dt = decltype(dtc)::value;
+      bf16x4* t = (dt & 1) ? tb : ta;
+      wait_tr<4, 0>(t);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        mfma32_agpr(dv0[dt], cat44(t[2 * s], t[2 * s + 1]), pb0[s]);
+        mfma32_agpr(dv1[dt], cat44(t[2 * s], t[2 * s + 1]), pb1[s]);
+      }
+      if constexpr (dt + 1 < DT) trr(o0, o1, std::integral_constant<int, dt + 1>{}, (dt & 1) ? ta : tb);
+      else trr(qa0, qa1, std::integral_constant<int, 0>{}, (dt & 1) ? ta : tb);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = 4 * dt + e;
+        p0[j] *= s0[j];
+        p1[j] *= s1[j];
+      }
+      sw0[dt >> 1][2 * (dt & 1)] = pack2(p0[4 * dt], p0[4 * dt + 1]);
+      sw0[dt >> 1][2 * (dt & 1) + 1] = pack2(p0[4 * dt + 2], p0[4 * dt + 3]);
+      sw1[dt >> 1][2 * (dt & 1)] = pack2(p1[4 * dt], p1[4 * dt + 1]);
+      sw1[dt >> 1][2 * (dt & 1) + 1] = pack2(p1[4 * dt + 2], p1[4 * dt + 3]);
+      if constexpr ((dt & 1) && (DIAG & 1)) asm volatile("" ::"v"(sw0[dt >> 1]), "v"(sw1[dt >> 1]));
+      if constexpr ((dt & 1) && !(DIAG & 1)) {
+        if constexpr (QM) {
+          stage_w<(dt >> 1)>(sw0[dt >> 1], (dt >> 1) ? stw1 : stw0, std::integral_constant<int, 0>{});
+          stage_w<(dt >> 1)>(sw1[dt >> 1], (dt >> 1) ? stw1 : stw0, std::integral_constant<int, 2048>{});
+        } else {
+          st(sw0[dt >> 1], row0, dt >> 1, dsoff);
+          st(sw1[dt >> 1], row1, dt >> 1, dsoff);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    st1 = (DIAG & 1) ? 0 : 4;
+    const bf16x8 sb0[2] = {__builtin_bit_cast(bf16x8, sw0[0]), __builtin_bit_cast(bf16x8, sw0[1])};
+    const bf16x8 sb1[2] = {__builtin_bit_cast(bf16x8, sw1[0]), __builtin_bit_cast(bf16x8, sw1[1])};
+    // ---- dK^T += Q^T.dS (16 MFMAs); QM: the staged dS tile goes out as whole lines, one store per step
+    const uint64_t dsq0 = dsq + 2ull * (uint64_t)qs0 * (uint64_t)S;
+    bf16x4 xa[2], xb[2];
+    static_for<DT>([&](auto dtc) {
+      constexpr int dt = decltype(dtc)::value;
+      bf16x4* t = ((DT + dt) & 1) ? tb : ta;  // Q^T block 0 went to the buffer after the last dO^T block
+      bf16x4* xc = (dt & 1) ? xb : xa;
+      bf16x4* xp = (dt & 1) ? xa : xb;
+      if constexpr (QM && !(DIAG & 1)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(xp[0]), "+v"(xp[1]));
+        if constexpr (dt > 0) stage_st<dt - 1, (DIAG & 16) != 0>(xp, dsq0, sqoff);
+      } else {
+        wait_tr<4, 0>(t);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        mfma32_agpr(dk0[dt], cat44(t[2 * s], t[2 * s + 1]), sb0[s]);
+        mfma32_agpr(dk1[dt], cat44(t[2 * s], t[2 * s + 1]), sb1[s]);
+      }
+      if constexpr (dt + 1 < DT) trr(qa0, qa1, std::integral_constant<int, dt + 1>{}, ((DT + dt) & 1) ? ta : tb);
+      if constexpr (QM && !(DIAG & 1)) {
+        xc[0] = lds_tr_read_off<1024 * dt>(str);
+        xc[1] = lds_tr_read_off<1024 * dt + 512>(str);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    if constexpr (QM && !(DIAG & 1)) {
+      bf16x4* xl = ((DT - 1) & 1) ? xb : xa;
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xl[0]), "+v"(xl[1]));
+      stage_st<DT - 1, (DIAG & 16) != 0>(xl, dsq0, sqoff);
+    }
+    asm volatile("" ::: "memory");
+  };
+  int qt = qt0;
+  if (causal) {
+    const int qd = qt0 + BN / BQ < nqt ? qt0 + BN / BQ : nqt;
+    for (; qt < qd; ++qt) body(qt, std::true_type{});
+  }
+  for (; qt < nqt; ++qt) body(qt, std::false_type{});
+  // the accumulators leave the AGPRs through compiler v_accvgpr_read: 18 wait states after the last 16-pass MFMA
+  // that wrote them (hipcc pads nothing after an asm MFMA)
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3"
+               : "+a"(dk0[0]), "+a"(dk0[1]), "+a"(dk0[2]), "+a"(dk0[3]), "+a"(dk1[0]), "+a"(dk1[1]), "+a"(dk1[2]),
+                 "+a"(dk1[3]), "+a"(dv0[0]), "+a"(dv0[1]), "+a"(dv0[2]), "+a"(dv0[3]), "+a"(dv1[0]), "+a"(dv1[1]),
+                 "+a"(dv1[2]), "+a"(dv1[3]));
+
+  auto out = [&](const f32x16* dka, const f32x16* dva, int key) {
+    if constexpr (DIRECT) {
+      bf16_t* dkb = reinterpret_cast<bf16_t*>(dk_part) + (int64_t)(b * S + key) * dks + hq * D;
+      bf16_t* dvb = reinterpret_cast<bf16_t*>(dv_part) + (int64_t)(b * S + key) * dvs + hq * D;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d = dt * 32 + 8 * g4 + 4 * hh;
+          *reinterpret_cast<u32x2*>(dkb + d) =
+              u32x2{pack2(dka[dt][4 * g4] * scale, dka[dt][4 * g4 + 1] * scale),
+                    pack2(dka[dt][4 * g4 + 2] * scale, dka[dt][4 * g4 + 3] * scale)};
+          *reinterpret_cast<u32x2*>(dvb + d) =
+              u32x2{pack2(dva[dt][4 * g4], dva[dt][4 * g4 + 1]), pack2(dva[dt][4 * g4 + 2], dva[dt][4 * g4 + 3])};
+        }
+      }
+    } else {
+      float* dkp = dk_part + (int64_t)(b * S + key) * Hq * D + hq * D;
+      float* dvp = dv_part + (int64_t)(b * S + key) * Hq * D + hq * D;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d = dt * 32 + 8 * g4 + 4 * hh;
+          *reinterpret_cast<f32x4*>(dkp + d) = f32x4{dka[dt][4 * g4] * scale, dka[dt][4 * g4 + 1] * scale,
+                                                     dka[dt][4 * g4 + 2] * scale, dka[dt][4 * g4 + 3] * scale};
+          *reinterpret_cast<f32x4*>(dvp + d) =
+              f32x4{dva[dt][4 * g4], dva[dt][4 * g4 + 1], dva[dt][4 * g4 + 2], dva[dt][4 * g4 + 3]};
+        }
+      }
+    }
+  };
+  out(dk0, dv0, k0w + r);
+  out(dk1, dv1, k0w + 32 + r);
+}
+
+void flash_attn_bwd_dkdv64(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout, const float* nlse,
+                           const float* ndelta, float* dk_part, float* dv_part, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B,
+                           int S, int Hq, int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t dos, int64_t dks,
+                           int64_t dvs, float scale, int causal, bool qm, hipStream_t stream) {
+  constexpr int D = 128, NS = 3;
+  const size_t lds = 256 * (D * 2) + NS * (2 * 32 * (D * 2) + 1024) + 4 * 4096;
+  const dim3 grid(B * Hq * (S / 256));
+  static const int diag = [] {
+    const char* e = getenv("KOP_DKDV64_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+  // one instantiation per (DIRECT, QM, DIAG) actually launched; the dynamic-LDS attribute is set on first use
+#define KOP_LAUNCH(DIR, QMV, DG)                                                                                    \
+  do {                                                                                                             \
+    static bool attr = false;                                                                                      \
+    if (!attr) {                                                                                                   \
+      (void)hipFuncSetAttribute((const void*)fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG>,                              \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                             \
+      attr = true;                                                                                                 \
+    }                                                                                                              \
+    if (DIR)                                                                                                       \
+      fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG><<<grid, 256, lds, stream>>>(                                        \
+          q, k, v, dout, nlse, ndelta, reinterpret_cast<float*>(dk), reinterpret_cast<float*>(dv), ds, B, S, Hq, Hkv, \
+          qs, ks, vs, dos, scale, causal, dks, dvs);                                                               \
+    else                                                                                                           \
+      fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG><<<grid, 256, lds, stream>>>(                                        \
+          q, k, v, dout, nlse, ndelta, dk_part, dv_part, ds, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal, 0, 0);  \
+  } while (0)
+  if (diag != 0 && Hq != Hkv && qm) {
+    switch (diag) {
+      case 1: KOP_LAUNCH(false, true, 1); return;
+      case 2: KOP_LAUNCH(false, true, 2); return;
+      case 4: KOP_LAUNCH(false, true, 4); return;
+      case 8: KOP_LAUNCH(false, true, 8); return;
+      case 16: KOP_LAUNCH(false, true, 16); return;
+      case 32: KOP_LAUNCH(false, true, 32); return;
+      case 48: KOP_LAUNCH(false, true, 48); return;
+      default: break;
+    }
+  }
+  if (Hq == Hkv) {
+    if (qm) KOP_LAUNCH(true, true, 0);
+    else KOP_LAUNCH(true, false, 0);
+  } else {
+    if (qm) KOP_LAUNCH(false, true, 0);
+    else KOP_LAUNCH(false, false, 0);
+  }
+#undef KOP_LAUNCH
+}
+
+}  // namespace kop

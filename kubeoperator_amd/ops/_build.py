@@ -58,6 +58,11 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError("build command failed:\n" + " ".join(cmd) + "\n" + res.stdout)
 
 
+# per-file hipcc flags: the one-wave-per-SIMD dK/dV kernel keeps its builtin MFMAs in VGPR form (its dK/dV
+# accumulators are AGPR inline-asm operands; hipcc's heuristic would put every MFMA in AGPR form)
+FILE_FLAGS = {"flash_bwd_w1.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=true"]}
+
+
 def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -> str:
     """Compile every kernel for gfx950 and link ``_C.so``; returns its path."""
     os.makedirs(BUILD_DIR, exist_ok=True)
@@ -73,7 +78,7 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         objs.append(obj)
         if force or _needs(obj, src, hdr):
             jobs_list.append([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics",
-                              abi, "-I", CSRC, "-c", src, "-o", obj])
+                              abi, *FILE_FLAGS.get(os.path.basename(src), []), "-I", CSRC, "-c", src, "-o", obj])
     bsrc = os.path.join(CSRC, "bindings.cpp")
     bobj = os.path.join(BUILD_DIR, "bindings.cpp.o")
     objs.append(bobj)

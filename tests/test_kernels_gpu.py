@@ -296,15 +296,20 @@ def test_weight_grad_tn_layout_matches_nt(layout, monkeypatch):
         assert rel_err(out, 2 * ref) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [10, 9, 8])
-@pytest.mark.parametrize("D,Hq,Hkv,S", [(128, 8, 2, 512), (64, 4, 4, 256), (128, 4, 1, 768), (128, 8, 1, 256), (64, 8, 4, 512)])
+@pytest.mark.parametrize("variant,cfg", [(10, 64), (10, 65), (10, 42), (9, 42), (8, 42)],
+                         ids=["ds-dkdv64", "ds_t-dkdv65", "ds-dkdv42", "recompute9", "recompute8"])
+@pytest.mark.parametrize("D,Hq,Hkv,S", [(128, 8, 2, 512), (64, 4, 4, 256), (128, 4, 1, 768), (128, 8, 1, 256),
+                                        (64, 8, 4, 512), (128, 4, 4, 512), (128, 6, 2, 512), (128, 2, 1, 256)])
 @pytest.mark.parametrize("causal", [True, False])
-def test_flash_attention_bwd_dq_variants(variant, D, Hq, Hkv, S, causal):
-    """every dQ algorithm (recompute 8/9, materialised dS 10) against the fp32 autograd reference."""
+def test_flash_attention_bwd_dq_variants(variant, cfg, D, Hq, Hkv, S, causal):
+    """every dQ algorithm (recompute 8/9, materialised dS 10) and dK/dV kernel (64 / 65: one wave per SIMD with the
+    query-major LDS-staged / transposed dS, D = 128; 42: two waves per SIMD) against the fp32 autograd reference. The shapes cover the
+    no-GQA direct path (Hq == Hkv) and every dQ head grouping (8, 4, 2, 1 heads per workgroup)."""
     from kubeoperator_amd.ops.functional import rope_attention
     from kubeoperator_amd.ops.reference import attention_ref
 
     old = lib().flash_attn_set_dq_variant(variant)
+    old_cfg = lib().flash_attn_set_dkdv_cfg(cfg)
     try:
         B = 2
         torch.manual_seed(12)
@@ -320,6 +325,7 @@ def test_flash_attention_bwd_dq_variants(variant, D, Hq, Hkv, S, causal):
             assert rel_err(qkv.grad[:, lo:hi], x.grad[:, lo:hi]) < 3e-2
     finally:
         lib().flash_attn_set_dq_variant(old)
+        lib().flash_attn_set_dkdv_cfg(old_cfg)
 
 
 @pytest.mark.parametrize("rows,H", [(8192, 768), (8192, 2304), (4096, 3072), (77, 24), (1000, 1024)])

@@ -12,6 +12,8 @@
 #   prof-gpt2    rocprofv3 kernel trace + stats of the GPT-2-small step
 #   pmc-attn     PMC counter passes (one rocprofv3 run each) over the attention micro-benchmark
 #   attn-probe   attention TF/s per shape; VARIANTS="ENV=a;ENV=b;base" alternates env variants twice
+#   attn-prof    rocprofv3 kernel trace of the attention probe per VARIANTS entry (per-kernel times), then PMC passes
+#                over the first entry
 #   dp           one-GPU data-parallel rehearsals (2 / 4 gloo ranks sharing cuda:0) + bench.py --gpus 2 under torchrun
 #   tp           one-GPU tensor (+ sequence) parallel rehearsals + bench.py --tp 2 [--sp 1] + 4 Llama-3-70B layers
 #   wgrad-lag    weight-gradient and optimizer streams under a forced lag: GPU tests, then DP / TP rehearsals
@@ -87,6 +89,22 @@ s_attn_probe() {
     done
   done
   cat $out
+}
+
+s_attn_prof() {
+  local v envs i=0 prog="python3 tools/attn_probe.py --shapes ${SHAPES:-llama} --causal 1 --iters 6"
+  IFS=';' read -ra VS <<< "${VARIANTS:-base}"
+  for v in "${VS[@]}"; do
+    i=$((i + 1)); [ "$v" = "base" ] && envs="" || envs="$v"
+    (export $envs; step attn_prof_$i 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/attn_$i -o attn_$i \
+      --output-format csv -- $prog) || return $?
+  done
+  v="${VS[0]}"; [ "$v" = "base" ] && envs="" || envs="$v"
+  (export $envs
+   pmc abusy "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS" $prog && \
+   pmc ainst "SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_WAVES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA SQ_WAIT_INST_ANY" $prog && \
+   pmc agrbm "GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD" $prog) && \
+  python tools/pmc_summary.py $(find gpurun_out/pmc -name '*counter_collection.csv') > gpurun_out/pmc_attn_summary.txt
 }
 
 rehearse() {  # nproc script args...: the rehearsal's JSON line is appended to gpurun_out/rehearsals.jsonl

@@ -500,10 +500,16 @@ int flash_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o,
   if (S % (32 * kFwdWaves) != 0 || Hq % Hkv != 0) return -1;
   if (qs % 8 || ks % 8 || vs % 8 || os % 8) return -2;
   const float sl2 = scale * 1.4426950408889634f;
-  static const int variant = [] {
+  // KOP_FWD_VARIANT: 8 lockstep 8-wave kernel (scalar-FMA softmax), 10 the same with packed FMAs, 9 staggered halves,
+  // < 8 the 4-wave kernel. Defaults per head dim from same-box probes (profiles/r3_fwd_variant_probe.jsonl): D = 128 ->
+  // 8 (2-3 % over 10: packed f32 VALU beside MFMAs is an anti-lever, MI355X_MICROARCH.md); D = 64 causal -> 4-wave
+  // (short causal sweeps, more workgroups per CU), non-causal -> 8.
+  static const int env_variant = [] {
     const char* e = getenv("KOP_FWD_VARIANT");
-    return e ? atoi(e) : 10;  // 10: lockstep 8-wave kernel with packed-FMA softmax (8: unpacked, 9: staggered)
+    return e ? atoi(e) : -1;
   }();
+  int variant = env_variant >= 0 ? env_variant : (D == 64 && causal) ? 0 : 8;
+  if (ot != nullptr && variant < 8) variant = 8;  // O^T comes only from the 8-wave kernel
   if (S % 256 == 0 && variant >= 8) {
     if (D == 128) {
       if (variant == 9) launch_fwd8<128, true>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream, ot);

@@ -112,13 +112,13 @@ def main() -> int:
 
     import torch
 
-    from kubeoperator_amd.parallel.dist import all_reduce_max, barrier, init_distributed, shutdown
+    from kubeoperator_amd.parallel.dist import all_reduce_max, barrier, collectives_on, init_distributed, shutdown
     from kubeoperator_amd.models import get_config
     from kubeoperator_amd.train import SyntheticTokens, TrainConfig, Trainer
 
     info = init_distributed(args.device, timeout_s=args.comm_timeout)
     if args.dp == "auto":
-        args.dp = "zero1" if info.world > 1 else "allreduce"
+        args.dp = "zero1" if collectives_on(info) else "allreduce"
     from kubeoperator_amd.train import gemm_tuning
 
     tuning = gemm_tuning.setup(args.gemm_tuning, rank=info.rank)
@@ -152,7 +152,7 @@ def main() -> int:
     sync()
     barrier(info)
     sync()
-    timing = cuda and world > 1
+    timing = cuda and collectives_on(info)
     if timing:  # exposed-communication events (a handful per step, no host synchronisation)
         trainer.dp.finish_waits, trainer.store.gate_waits = [], []
     comm0, gather0 = trainer.dp.comm_bytes, trainer.dp.gather_bytes
@@ -209,7 +209,7 @@ def main() -> int:
                 "seq_len": args.seq,
                 "parallelism": (f"tp{args.tp}-" if args.tp > 1 else "") + ("sp-" if args.sp and args.tp > 1 else "")
                 + f"dp{dp_world}"
-                + ("-zero1" if args.dp == "zero1" and dp_world > 1 else ""),
+                + ("-zero1" if args.dp == "zero1" and (dp_world > 1 or collectives_on(info)) else ""),
                 "optimizer": "fused AdamW (fp32 master/moments), grad clip 1.0",
                 "optimizer_overlap": bool(args.overlap_opt),
                 "hip_graph": bool(args.cuda_graph),

@@ -26,7 +26,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops.optim import Segment
-from .dist import DistInfo
+from .dist import DistInfo, collectives_on
 from .flat import Bucket, FlatParamStore
 
 
@@ -57,6 +57,8 @@ class DataParallel:
         self.finish_waits: list | None = None  # (event, event) around finish_grads (exposed comm timing)
         store.on_ready = self._on_ready
         self.overlapped = False  # set once the optimizer publishes ZeRO-1 gathers itself
+        # one-rank RCCL self-test (parallel.dist.rccl_selftest): world-1 buckets still go through the collectives
+        self.force = info.world == 1 and collectives_on(info)
 
     def _topo(self, b: Bucket):
         """(group, rank, world) the bucket's gradient collective and ZeRO-1 pieces run over."""
@@ -66,12 +68,12 @@ class DataParallel:
 
     # -------------------------------------------------------------------------------------------
     def broadcast_params(self) -> None:
-        if self.world > 1:
+        if self.world > 1 or self.force:
             dist.broadcast(self.store.params, src=self.info.src, group=self.group)
 
     def _on_ready(self, b: Bucket) -> None:
         group, rank, world = self._topo(b)
-        if world == 1 or not self.sync:
+        if (world == 1 and not self.force) or not self.sync:
             return
         g = self.store.grads[b.start:b.end]
         self.comm_bytes += g.numel() * g.element_size()
@@ -123,7 +125,7 @@ class DataParallel:
             return None
         b = self.store.buckets[seg.bucket]
         group, rank, world = self._topo(b)
-        if world == 1:
+        if world == 1 and not self.force:
             return None
         self.overlapped = True
         a, e = b.piece(rank, world)
@@ -145,7 +147,7 @@ class DataParallel:
         """The grad-norm sum of squares is summed over the ranks holding distinct gradient pieces: the DP
         group under ZeRO-1, the TP group under tensor parallelism, the whole job with both."""
         tp = self.tp is not None and self.tp.enabled
-        if self.mode == "zero1" and (self.world > 1 or self.sp):
+        if self.mode == "zero1" and (self.world > 1 or self.sp or self.force):
             if tp:
                 return lambda t: dist.all_reduce(t)  # every rank: DP pieces x TP shards
             return lambda t: dist.all_reduce(t, group=self.group)
@@ -160,7 +162,7 @@ class DataParallel:
         st = self.store
         for b in st.buckets:
             group, rank, world = self._topo(b)
-            if world == 1:
+            if world == 1 and not self.force:
                 continue
             a, e = b.piece(rank, world)
             w = self._gather(b, a, e, group, async_op=True)

@@ -31,6 +31,20 @@ class DistInfo:
         return self.rank == 0
 
 
+def rccl_selftest() -> bool:
+    """``KOP_RCCL_SELFTEST=1`` under torchrun: even a one-rank job builds its process group and runs every
+    data-parallel collective (the gradient reduce-scatter / all-reduce, the ZeRO-1 all-gathers, the grad-norm
+    all-reduce, barriers) through the backend -- the RCCL code path of the multi-GPU bench, executed on a one-GPU
+    box. A one-rank collective moves no bytes over xGMI but goes through RCCL's launch, stream and in-place
+    argument handling exactly as at world size 8."""
+    return os.environ.get("KOP_RCCL_SELFTEST") == "1" and "MASTER_ADDR" in os.environ
+
+
+def collectives_on(info: "DistInfo") -> bool:
+    """Whether this job runs its collectives: more than one rank, or the one-rank RCCL self-test."""
+    return info.world > 1 or (info.backend not in ("none", "") and rccl_selftest())
+
+
 def init_distributed(device: str = "auto", timeout_s: int = 1800) -> DistInfo:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -44,7 +58,7 @@ def init_distributed(device: str = "auto", timeout_s: int = 1800) -> DistInfo:
     else:
         dev = torch.device("cpu")
     backend = "none"
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or rccl_selftest()) and not dist.is_initialized():
         backend = os.environ.get("KOP_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
@@ -73,7 +87,7 @@ def init_distributed(device: str = "auto", timeout_s: int = 1800) -> DistInfo:
 
 
 def barrier(info: DistInfo) -> None:
-    if info.world > 1:
+    if collectives_on(info):
         if info.backend == "nccl":
             dist.barrier(group=info.group, device_ids=[info.local_rank])
         else:
@@ -81,7 +95,7 @@ def barrier(info: DistInfo) -> None:
 
 
 def all_reduce_max(x: float, info: DistInfo) -> float:
-    if info.world == 1:
+    if not collectives_on(info):
         return x
     t = torch.tensor([x], dtype=torch.float64, device=info.device if info.backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=info.group)
@@ -89,7 +103,7 @@ def all_reduce_max(x: float, info: DistInfo) -> float:
 
 
 def all_reduce_sum(x: float, info: DistInfo) -> float:
-    if info.world == 1:
+    if not collectives_on(info):
         return x
     t = torch.tensor([x], dtype=torch.float64, device=info.device if info.backend == "nccl" else "cpu")
     dist.all_reduce(t, group=info.group)
@@ -97,5 +111,5 @@ def all_reduce_sum(x: float, info: DistInfo) -> float:
 
 
 def shutdown(info: DistInfo) -> None:
-    if info.world > 1 and dist.is_initialized():
+    if dist.is_initialized():
         dist.destroy_process_group()

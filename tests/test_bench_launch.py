@@ -65,3 +65,23 @@ def test_bench_refuses_mismatched_world():
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode != 0
     assert not _json_lines(p.stdout)
+
+
+def test_one_rank_collective_selftest_runs_the_dp_path():
+    """KOP_RCCL_SELFTEST=1 under torchrun: a one-rank job builds its process group (gloo here, RCCL on a GPU box) and
+    every data-parallel collective runs: ZeRO-1 reduce-scatter + all-gather bytes are counted, exposed time is
+    measured, and the step matches the plain one-rank job's loss."""
+    env = _env()
+    env["KOP_RCCL_SELFTEST"] = "1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", _port(), "bench.py", "--gpus", "1"] + ARGS
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1
+    r = lines[0]
+    assert r["n_gpus"] == 1 and r["rccl_world"] == 1 and r["backend"] == "gloo"
+    assert r["config"]["parallelism"] == "dp1-zero1"
+    assert r["grad_comm_bytes_per_step"] > 0 and r["param_gather_bytes_per_step"] > 0
+    plain = _run([sys.executable, "bench.py", "--gpus", "1"] + ARGS)[0]
+    assert abs(plain["last_loss"] - r["last_loss"]) < 1e-3, (plain["last_loss"], r["last_loss"])

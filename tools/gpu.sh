@@ -14,6 +14,8 @@
 #   attn-probe   attention TF/s per shape; VARIANTS="ENV=a;ENV=b;base" alternates env variants twice
 #   attn-prof    rocprofv3 kernel trace of the attention probe per VARIANTS entry (per-kernel times), then PMC passes
 #                over the first entry
+#   rccl1        one-rank RCCL self-test (KOP_RCCL_SELFTEST=1): the bench's data-parallel collectives through RCCL
+#                under torchrun on one GPU -- 1B proxy (ZeRO-1, all-reduce) and Llama-3-8B (ZeRO-1)
 #   dp           one-GPU data-parallel rehearsals (2 / 4 gloo ranks sharing cuda:0) + bench.py --gpus 2 under torchrun
 #   tp           one-GPU tensor (+ sequence) parallel rehearsals + bench.py --tp 2 [--sp 1] + 4 Llama-3-70B layers
 #   wgrad-lag    weight-gradient and optimizer streams under a forced lag: GPU tests, then DP / TP rehearsals
@@ -110,6 +112,16 @@ s_attn_prof() {
 rehearse() {  # nproc script args...: the rehearsal's JSON line is appended to gpurun_out/rehearsals.jsonl
   local n=$1; shift
   torchrun_n "reh_$((port + 1))" 300 "$n" "$@" && grep -h rehearsal "gpurun_out/reh_$port.log" | tee -a gpurun_out/rehearsals.jsonl
+}
+
+s_rccl1() {
+  export KOP_RCCL_SELFTEST=1
+  torchrun_n rccl1_zero1 300 1 bench.py --gpus 1 --steps 3 --warmup 1 --model llama3_1b_proxy --seq 2048 && \
+  torchrun_n rccl1_allreduce 300 1 bench.py --gpus 1 --steps 3 --warmup 1 --model llama3_1b_proxy --seq 2048 \
+    --dp allreduce && \
+  torchrun_n rccl1_l8b 400 1 bench.py --gpus 1 --steps 5 --warmup 2 && \
+  grep -h '"metric"' gpurun_out/rccl1_*.log | tee gpurun_out/rccl1.jsonl
+  local rc=$?; unset KOP_RCCL_SELFTEST; return $rc
 }
 
 s_dp() {

@@ -1107,8 +1107,16 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
     if (!direct) fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs);
     return;
   }
-  fa_bwd_dkdv_kernel<D, NW, false><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(
-      q, k, v, dout, nlse, ndelta, dk_part, dv_part, nullptr, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);
+  if (D == 128 && dkdv_cfg() == 64 && S % 256 == 0) {
+    // the one-wave dK/dV kernel without dS stores; dQ recomputes S and dP below. It writes bf16 dK / dV itself
+    // when Hq == Hkv, so the finalize pass is then skipped.
+    flash_attn_bwd_dkdv64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, nullptr, B, S, Hq, Hkv, qs, ks, vs,
+                          dos, dks, dvs, scale, causal ? 1 : 0, false, stream);
+  } else {
+    fa_bwd_dkdv_kernel<D, NW, false><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(
+        q, k, v, dout, nlse, ndelta, dk_part, dv_part, nullptr, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);
+  }
+  const bool direct64 = D == 128 && dkdv_cfg() == 64 && S % 256 == 0 && Hq == Hkv;
   if (S % 256 == 0 && variant >= 8) {
     const bool stg = variant != 8;
     const size_t lds8 = (stg ? 4 : 3) * 2 * 64 * (D * 2);
@@ -1130,7 +1138,7 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
     fa_bwd_dq_kernel<D, NW><<<B * Hq * (S / (32 * NW)), NW * 64, lds_q, stream>>>(
         q, k, v, dout, lse, delta, dq, B, S, Hq, Hkv, qs, ks, vs, dos, dqs, scale, causal);
   }
-  fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs);
+  if (!direct64) fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs);
 }
 
 int flash_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,

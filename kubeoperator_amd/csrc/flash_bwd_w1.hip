@@ -83,8 +83,9 @@ __device__ __forceinline__ void vm_wait_le(int n) {
 }
 #undef KOP_VM_CASE
 
-// DIAG (timing ablations, KOP_DKDV64_DIAG): 1 no dS stores, 2 no exponentials, 4 no stage DMA, 8 no stage barrier,
-// 32 no DMA wait (all of these give wrong results); 16 non-temporal dS stores (correct)
+// DIAG bit 1: no dS stores -- the build the recompute-dQ path (KOP_DQ_VARIANT 9) launches. Timing ablations
+// (KOP_DKDV64_DIAG, wrong results): 2 no exponentials, 4 no stage DMA, 8 no stage barrier, 32 no DMA wait; 16
+// non-temporal dS stores (correct, slower).
 // QM: dS in the query-major layout of fa_bwd_dkdv_kernel ([B, Hq, query, slot(key)]), staged through LDS so each
 // wave writes whole 128-B lines (its 64 keys are one line of every query row); else transposed, stored directly.
 template <int D, bool DIRECT, int NS, bool QM, int DIAG = 0>
@@ -459,7 +460,7 @@ void flash_attn_bwd_dkdv64(const bf16_t* q, const bf16_t* k, const bf16_t* v, co
       fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG><<<grid, 256, lds, stream>>>(                                        \
           q, k, v, dout, nlse, ndelta, dk_part, dv_part, ds, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal, 0, 0);  \
   } while (0)
-  if (diag != 0 && Hq != Hkv && qm) {
+  if (diag != 0 && Hq != Hkv && qm && ds != nullptr) {
     switch (diag) {
       case 1: KOP_LAUNCH(false, true, 1); return;
       case 2: KOP_LAUNCH(false, true, 2); return;
@@ -471,7 +472,10 @@ void flash_attn_bwd_dkdv64(const bf16_t* q, const bf16_t* k, const bf16_t* v, co
       default: break;
     }
   }
-  if (Hq == Hkv) {
+  if (ds == nullptr) {  // no dS at all (dQ recomputes it): the store-free build
+    if (Hq == Hkv) KOP_LAUNCH(true, true, 1);
+    else KOP_LAUNCH(false, true, 1);
+  } else if (Hq == Hkv) {
     if (qm) KOP_LAUNCH(true, true, 0);
     else KOP_LAUNCH(true, false, 0);
   } else {

@@ -296,8 +296,8 @@ def test_weight_grad_tn_layout_matches_nt(layout, monkeypatch):
         assert rel_err(out, 2 * ref) < 1e-2
 
 
-@pytest.mark.parametrize("variant,cfg", [(10, 64), (10, 65), (10, 42), (9, 42), (8, 42)],
-                         ids=["ds-dkdv64", "ds_t-dkdv65", "ds-dkdv42", "recompute9", "recompute8"])
+@pytest.mark.parametrize("variant,cfg", [(10, 64), (10, 65), (10, 42), (9, 64), (9, 42), (8, 42)],
+                         ids=["ds-dkdv64", "ds_t-dkdv65", "ds-dkdv42", "recompute9-dkdv64", "recompute9", "recompute8"])
 @pytest.mark.parametrize("D,Hq,Hkv,S", [(128, 8, 2, 512), (64, 4, 4, 256), (128, 4, 1, 768), (128, 8, 1, 256),
                                         (64, 8, 4, 512), (128, 4, 4, 512), (128, 6, 2, 512), (128, 2, 1, 256)])
 @pytest.mark.parametrize("causal", [True, False])

@@ -791,7 +791,9 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq8_kernel(
 // group a lane's B fragment dS^T is one ds_read_b128 of its row (keys are stored in MFMA order, ds_slot),
 // and dQ^T += K^T . dS^T accumulates in DT independent chains. The dS stream (half of B*Hq*S*S bf16 under
 // a causal mask) makes this kernel HBM-bound, ~3x cheaper than recomputing.
-template <int D, int HP>
+// BLK: dS in the wave-block layout of fa_bwd_dkdv64_kernel ([B, Hq, S/32, S/64, 32 queries, 64 slots]); the
+// tile's dS rows of one head and 32-query stage are then one contiguous 4-KB block.
+template <int D, int HP, bool BLK = false>
 __global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __restrict__ ds, const bf16_t* __restrict__ k,
                                                               bf16_t* __restrict__ dq, int B, int S, int Hq, int Hkv,
                                                               int64_t ks, int64_t dqs, float scale, int causal) {
@@ -827,7 +829,11 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __re
       const int piece = wid + i * NW;
       const int row = 8 * piece + lrow;
       const int ch = 4 * lhi + (lslot ^ ((row >> 2) & 3));
-      const bf16_t* src = ds + ((int64_t)(b * Hq + hg * HP + row / RH) * S + q0 + row % RH) * S + t * BN + ch * 8;
+      const int qrow = q0 + row % RH;
+      const bf16_t* src =
+          BLK ? ds + (((int64_t)(b * Hq + hg * HP + row / RH) * (S / 32) + qrow / 32) * (S / 64) + t) * 2048 +
+                    (qrow % 32) * 64 + ch * 8
+              : ds + ((int64_t)(b * Hq + hg * HP + row / RH) * S + qrow) * S + t * BN + ch * 8;
       glds16(src, sl + KT + piece * 1024);
     }
   };
@@ -900,18 +906,18 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __re
   }
 }
 
-template <int D, int HP>
+template <int D, int HP, bool BLK = false>
 static void launch_dq_ds(const bf16_t* ds, const bf16_t* k, bf16_t* dq, int B, int S, int Hq, int Hkv, int64_t ks,
                          int64_t dqs, float scale, bool causal, hipStream_t stream) {
   const size_t lds = 3 * (64 * (D * 2) + 256 * 64 * 2);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)fa_bwd_dq_ds_kernel<D, HP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
+    (void)hipFuncSetAttribute((const void*)fa_bwd_dq_ds_kernel<D, HP, BLK>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  fa_bwd_dq_ds_kernel<D, HP><<<B * (Hq / HP) * (S / (256 / HP)), 512, lds, stream>>>(ds, k, dq, B, S, Hq, Hkv, ks,
-                                                                                    dqs, scale, causal);
+  fa_bwd_dq_ds_kernel<D, HP, BLK><<<B * (Hq / HP) * (S / (256 / HP)), 512, lds, stream>>>(ds, k, dq, B, S, Hq, Hkv,
+                                                                                         ks, dqs, scale, causal);
 }
 
 // dk/dv = bf16(sum over the GQA group of the per-q-head partials)
@@ -1065,21 +1071,30 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
     const int hp = (grp % 8 == 0) ? 8 : (grp % 4 == 0) ? 4 : (grp % 2 == 0) ? 2 : 1;
     bool done = false;
     if constexpr (D == 128) {  // 8 waves need >= 8 1-KiB pieces per Q / dO tile (32 rows x 256 B)
-      if (cfg == 64 && S % 256 == 0) {
-        // one wave per SIMD, query-major dS staged through LDS (whole-line stores): the usual dQ kernel reads it
+      if ((cfg == 64 || cfg == 66) && S % 256 == 0) {
+        // one wave per SIMD, query-major dS staged through LDS (whole-line stores) -- in the wave-block layout (64)
+        // or plain rows (66) -- read by the materialised-dS dQ kernel
+        const bool blk = cfg == 64;
         flash_attn_bwd_dkdv64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs,
-                              dos, dks, dvs, scale, cflag, true, stream);
-        if (hp == 8) launch_dq_ds<D, 8>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-        else if (hp == 4) launch_dq_ds<D, 4>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-        else if (hp == 2) launch_dq_ds<D, 2>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-        else launch_dq_ds<D, 1>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+                              dos, dks, dvs, scale, cflag, true, blk, stream);
+        if (blk) {
+          if (hp == 8) launch_dq_ds<D, 8, true>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+          else if (hp == 4) launch_dq_ds<D, 4, true>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+          else if (hp == 2) launch_dq_ds<D, 2, true>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+          else launch_dq_ds<D, 1, true>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+        } else {
+          if (hp == 8) launch_dq_ds<D, 8>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+          else if (hp == 4) launch_dq_ds<D, 4>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+          else if (hp == 2) launch_dq_ds<D, 2>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+          else launch_dq_ds<D, 1>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+        }
         if (!direct) fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs);
         return;
       }
       if (cfg == 65 && S % 256 == 0) {
         // transposed dS (direct 16-B stores, half lines per stage): the dQ kernel that reads it
         flash_attn_bwd_dkdv64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs,
-                              dos, dks, dvs, scale, cflag, false, stream);
+                              dos, dks, dvs, scale, cflag, false, false, stream);
         if (hp == 8) launch_dq_dst<D, 8>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
         else if (hp == 4) launch_dq_dst<D, 4>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
         else if (hp == 2) launch_dq_dst<D, 2>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
@@ -1111,7 +1126,7 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
     // the one-wave dK/dV kernel without dS stores; dQ recomputes S and dP below. It writes bf16 dK / dV itself
     // when Hq == Hkv, so the finalize pass is then skipped.
     flash_attn_bwd_dkdv64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, nullptr, B, S, Hq, Hkv, qs, ks, vs,
-                          dos, dks, dvs, scale, causal ? 1 : 0, false, stream);
+                          dos, dks, dvs, scale, causal ? 1 : 0, false, false, stream);
   } else {
     fa_bwd_dkdv_kernel<D, NW, false><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(
         q, k, v, dout, nlse, ndelta, dk_part, dv_part, nullptr, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);

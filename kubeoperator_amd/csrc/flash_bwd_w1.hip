@@ -88,7 +88,9 @@ __device__ __forceinline__ void vm_wait_le(int n) {
 // non-temporal dS stores (correct, slower).
 // QM: dS in the query-major layout of fa_bwd_dkdv_kernel ([B, Hq, query, slot(key)]), staged through LDS so each
 // wave writes whole 128-B lines (its 64 keys are one line of every query row); else transposed, stored directly.
-template <int D, bool DIRECT, int NS, bool QM, int DIAG = 0>
+// BLK (with QM): wave-block dS layout [B, Hq, S/32, S/64, 32 queries, 64 slots]: a wave's stage tile is one contiguous
+// 4 KB block (its workgroup's stage: 16 KB), instead of 32 rows of 128 B spread 2*S bytes apart.
+template <int D, bool DIRECT, int NS, bool QM, int DIAG = 0, bool BLK = false>
 __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ nlse, const float* __restrict__ ndelta,
@@ -175,8 +177,10 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
   const int sg = lane >> 4, si = lane & 15, sq = si >> 2, sp = si & 3;
   const int skey = 4 * (sg >> 1) + sq;
   const uint32_t str = lds_addr(stg) + 64 * skey + 16 * ((2 * (sg & 1) + (sp >> 1)) ^ ((skey >> 1) & 3)) + 8 * (sp & 1);
-  const uint64_t dsq = (uint64_t)(uintptr_t)(dst + ((int64_t)(b * Hq + hq) * S) * S + k0w);
-  const uint32_t sqoff = 2u * (uint32_t)((16 * (sg & 1) + si) * S + 8 * (sg >> 1));
+  const uint64_t dsq = BLK ? (uint64_t)(uintptr_t)(dst + ((int64_t)(b * Hq + hq) * (S / 32) * (S / 64) + k0w / 64) * 2048)
+                          : (uint64_t)(uintptr_t)(dst + ((int64_t)(b * Hq + hq) * S) * S + k0w);
+  const uint32_t sqoff = BLK ? 2u * (uint32_t)((16 * (sg & 1) + si) * 64 + 8 * (sg >> 1))
+                             : 2u * (uint32_t)((16 * (sg & 1) + si) * S + 8 * (sg >> 1));
   (void)stw0; (void)stw1; (void)str; (void)dsq; (void)sqoff;
 
   auto body = [&](int qt, auto mask_c) {
@@ -351,7 +355,7 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     const bf16x8 sb0[2] = {__builtin_bit_cast(bf16x8, sw0[0]), __builtin_bit_cast(bf16x8, sw0[1])};
     const bf16x8 sb1[2] = {__builtin_bit_cast(bf16x8, sw1[0]), __builtin_bit_cast(bf16x8, sw1[1])};
     // ---- dK^T += Q^T.dS (16 MFMAs); QM: the staged dS tile goes out as whole lines, one store per step
-    const uint64_t dsq0 = dsq + 2ull * (uint64_t)qs0 * (uint64_t)S;
+    const uint64_t dsq0 = BLK ? dsq + 4096ull * (uint64_t)qt * (uint64_t)(S / 64) : dsq + 2ull * (uint64_t)qs0 * (uint64_t)S;
     bf16x4 xa[2], xb[2];
     static_for<DT>([&](auto dtc) {
       constexpr int dt = decltype(dtc)::value;
@@ -435,7 +439,7 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
 void flash_attn_bwd_dkdv64(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout, const float* nlse,
                            const float* ndelta, float* dk_part, float* dv_part, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B,
                            int S, int Hq, int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t dos, int64_t dks,
-                           int64_t dvs, float scale, int causal, bool qm, hipStream_t stream) {
+                           int64_t dvs, float scale, int causal, bool qm, bool blk_layout, hipStream_t stream) {
   constexpr int D = 128, NS = 3;
   const size_t lds = 256 * (D * 2) + NS * (2 * 32 * (D * 2) + 1024) + 4 * 4096;
   const dim3 grid(B * Hq * (S / 256));
@@ -444,43 +448,45 @@ void flash_attn_bwd_dkdv64(const bf16_t* q, const bf16_t* k, const bf16_t* v, co
     return e ? atoi(e) : 0;
   }();
   // one instantiation per (DIRECT, QM, DIAG) actually launched; the dynamic-LDS attribute is set on first use
-#define KOP_LAUNCH(DIR, QMV, DG)                                                                                    \
+#define KOP_LAUNCH(DIR, QMV, DG, BL)                                                                                    \
   do {                                                                                                             \
     static bool attr = false;                                                                                      \
     if (!attr) {                                                                                                   \
-      (void)hipFuncSetAttribute((const void*)fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG>,                              \
+      (void)hipFuncSetAttribute((const void*)fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG, BL>,                              \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                             \
       attr = true;                                                                                                 \
     }                                                                                                              \
     if (DIR)                                                                                                       \
-      fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG><<<grid, 256, lds, stream>>>(                                        \
+      fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG, BL><<<grid, 256, lds, stream>>>(                                    \
           q, k, v, dout, nlse, ndelta, reinterpret_cast<float*>(dk), reinterpret_cast<float*>(dv), ds, B, S, Hq, Hkv, \
           qs, ks, vs, dos, scale, causal, dks, dvs);                                                               \
     else                                                                                                           \
-      fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG><<<grid, 256, lds, stream>>>(                                        \
+      fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG, BL><<<grid, 256, lds, stream>>>(                                    \
           q, k, v, dout, nlse, ndelta, dk_part, dv_part, ds, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal, 0, 0);  \
   } while (0)
   if (diag != 0 && Hq != Hkv && qm && ds != nullptr) {
     switch (diag) {
-      case 1: KOP_LAUNCH(false, true, 1); return;
-      case 2: KOP_LAUNCH(false, true, 2); return;
-      case 4: KOP_LAUNCH(false, true, 4); return;
-      case 8: KOP_LAUNCH(false, true, 8); return;
-      case 16: KOP_LAUNCH(false, true, 16); return;
-      case 32: KOP_LAUNCH(false, true, 32); return;
-      case 48: KOP_LAUNCH(false, true, 48); return;
+      case 1: KOP_LAUNCH(false, true, 1, false); return;
+      case 2: KOP_LAUNCH(false, true, 2, false); return;
+      case 4: KOP_LAUNCH(false, true, 4, false); return;
+      case 8: KOP_LAUNCH(false, true, 8, false); return;
+      case 16: KOP_LAUNCH(false, true, 16, false); return;
+      case 32: KOP_LAUNCH(false, true, 32, false); return;
+      case 48: KOP_LAUNCH(false, true, 48, false); return;
       default: break;
     }
   }
   if (ds == nullptr) {  // no dS at all (dQ recomputes it): the store-free build
-    if (Hq == Hkv) KOP_LAUNCH(true, true, 1);
-    else KOP_LAUNCH(false, true, 1);
+    if (Hq == Hkv) KOP_LAUNCH(true, true, 1, false);
+    else KOP_LAUNCH(false, true, 1, false);
   } else if (Hq == Hkv) {
-    if (qm) KOP_LAUNCH(true, true, 0);
-    else KOP_LAUNCH(true, false, 0);
+    if (qm && blk_layout) KOP_LAUNCH(true, true, 0, true);
+    else if (qm) KOP_LAUNCH(true, true, 0, false);
+    else KOP_LAUNCH(true, false, 0, false);
   } else {
-    if (qm) KOP_LAUNCH(false, true, 0);
-    else KOP_LAUNCH(false, false, 0);
+    if (qm && blk_layout) KOP_LAUNCH(false, true, 0, true);
+    else if (qm) KOP_LAUNCH(false, true, 0, false);
+    else KOP_LAUNCH(false, false, 0, false);
   }
 #undef KOP_LAUNCH
 }

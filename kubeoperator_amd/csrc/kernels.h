@@ -77,11 +77,11 @@ size_t flash_attn_bwd_workspace(int B, int S, int Hq, int D);
 int flash_attn_set_dq_variant(int v);
 int flash_attn_set_dkdv_cfg(int c);
 // one-wave-per-SIMD dK/dV kernel (flash_bwd_w1.hip), D = 128, S % 256 == 0; writes dS query-major (qm: the
-// layout fa_bwd_dq_ds_kernel reads) or transposed (fa_bwd_dq_dst_kernel)
+// layout fa_bwd_dq_ds_kernel reads; blk_layout: its wave-block form) or transposed (fa_bwd_dq_dst_kernel)
 void flash_attn_bwd_dkdv64(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout, const float* nlse,
                            const float* ndelta, float* dk_part, float* dv_part, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B,
                            int S, int Hq, int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t dos, int64_t dks,
-                           int64_t dvs, float scale, int causal, bool qm, hipStream_t stream);
+                           int64_t dvs, float scale, int causal, bool qm, bool blk_layout, hipStream_t stream);
 int flash_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
                    const float* lse, bf16_t* dq, bf16_t* dk, bf16_t* dv, void* workspace, int B, int S, int Hq,
                    int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, int64_t dos, int64_t dqs,

@@ -520,5 +520,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flash_attn_bwd_workspace", &flash_attn_bwd_workspace);
   m.def("flash_attn_bwd", &flash_attn_bwd);
   m.def("flash_attn_set_dq_variant", [](int64_t v) { return (int64_t)kop::flash_attn_set_dq_variant((int)v); });
+  m.def("flash_attn_set_fwd_variant", [](int64_t v) { return (int64_t)kop::flash_attn_set_fwd_variant((int)v); });
   m.def("flash_attn_set_dkdv_cfg", [](int64_t c) { return (int64_t)kop::flash_attn_set_dkdv_cfg((int)c); });
 }

@@ -494,6 +494,17 @@ static void launch_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t
   fa_fwd_kernel<D, NW><<<grid, NW * 64, lds, stream>>>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal);
 }
 
+static int g_fwd_variant = -2;  // -2: read KOP_FWD_VARIANT on first use; -1: per-head-dim default
+int flash_attn_set_fwd_variant(int v) {
+  if (g_fwd_variant == -2) {
+    const char* e = getenv("KOP_FWD_VARIANT");
+    g_fwd_variant = e ? atoi(e) : -1;
+  }
+  const int old = g_fwd_variant;
+  if (v >= -1) g_fwd_variant = v;
+  return old;
+}
+
 int flash_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int S, int Hq,
                    int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, float scale, bool causal,
                    hipStream_t stream, bf16_t* ot) {
@@ -504,10 +515,7 @@ int flash_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o,
   // < 8 the 4-wave kernel. Defaults per head dim from same-box probes (profiles/r3_fwd_variant_probe.jsonl): D = 128 ->
   // 8 (2-3 % over 10: packed f32 VALU beside MFMAs is an anti-lever, MI355X_MICROARCH.md); D = 64 causal -> 4-wave
   // (short causal sweeps, more workgroups per CU), non-causal -> 8.
-  static const int env_variant = [] {
-    const char* e = getenv("KOP_FWD_VARIANT");
-    return e ? atoi(e) : -1;
-  }();
+  const int env_variant = flash_attn_set_fwd_variant(-3);  // current setting (-3 changes nothing)
   int variant = env_variant >= 0 ? env_variant : (D == 64 && causal) ? 0 : 8;
   if (ot != nullptr && variant < 8) variant = 8;  // O^T comes only from the 8-wave kernel
   if (S % 256 == 0 && variant >= 8) {

@@ -76,6 +76,9 @@ size_t flash_attn_bwd_workspace(int B, int S, int Hq, int D);
 // v < 0 only queries; returns the previous value. The workspace size depends on it.
 int flash_attn_set_dq_variant(int v);
 int flash_attn_set_dkdv_cfg(int c);
+// forward kernel variant: -1 per-head-dim default, 8 / 9 / 10 the 8-wave kernel, < 8 the 4-wave kernel; returns the old
+// setting (an argument below -1 only reads it)
+int flash_attn_set_fwd_variant(int v);
 // one-wave-per-SIMD dK/dV kernel (flash_bwd_w1.hip), D = 128, S % 256 == 0; writes dS query-major (qm: the
 // layout fa_bwd_dq_ds_kernel reads; blk_layout: its wave-block form) or transposed (fa_bwd_dq_dst_kernel)
 void flash_attn_bwd_dkdv64(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout, const float* nlse,

@@ -208,19 +208,56 @@ def test_flash_attention_fwd(D, causal):
     assert (lse - lse_ref).abs().max().item() < 2e-2
 
 
-def test_flash_attention_fwd_spiked_rescale():
-    """force the online-softmax rescale branch: a large score late in the key sweep."""
+@pytest.mark.parametrize("variant", [-1, 10, 8, 9, 0])
+def test_flash_attention_fwd_spiked_rescale(variant):
+    """force the online-softmax rescale branch: a large score late in the key sweep (every forward kernel:
+    -1 the default, 8 / 9 / 10 the 8-wave kernel, 0 the 4-wave kernel)."""
     from kubeoperator_amd.ops.functional import flash_attention
     from kubeoperator_amd.ops.reference import attention_ref
 
-    B, S, Hq, Hkv, D = 1, 512, 4, 4, 128
-    torch.manual_seed(8)
-    qkv = (0.3 * torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV)).to(torch.bfloat16)
-    a, c = Hq * D, (Hq + Hkv) * D
-    qkv[300, a:a + D] = qkv[400, :D] * 8  # key 300 aligns strongly with query 400
-    o, lse = flash_attention(qkv[:, :a], qkv[:, a:c], qkv[:, c:], B, S, Hq, Hkv, D, True)
-    o_ref, lse_ref = attention_ref(qkv[:, :a], qkv[:, a:c], qkv[:, c:], B, S, Hq, Hkv, D, True)
-    assert rel_err(o, o_ref) < 2e-2
+    old = lib().flash_attn_set_fwd_variant(variant)
+    try:
+        B, S, Hq, Hkv, D = 1, 512, 4, 4, 128
+        torch.manual_seed(8)
+        qkv = (0.3 * torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV)).to(torch.bfloat16)
+        a, c = Hq * D, (Hq + Hkv) * D
+        qkv[300, a:a + D] = qkv[400, :D] * 8  # key 300 aligns strongly with query 400
+        o, lse = flash_attention(qkv[:, :a], qkv[:, a:c], qkv[:, c:], B, S, Hq, Hkv, D, True)
+        o_ref, lse_ref = attention_ref(qkv[:, :a], qkv[:, a:c], qkv[:, c:], B, S, Hq, Hkv, D, True)
+        assert rel_err(o, o_ref) < 2e-2
+        assert (lse - lse_ref).abs().max().item() < 2e-2
+    finally:
+        lib().flash_attn_set_fwd_variant(old)
+
+
+@pytest.mark.parametrize("variant", [8, 10])
+@pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 512, 8, 2), (1, 1024, 4, 4), (2, 256, 6, 3)])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_fwd_variants_d128(variant, B, S, Hq, Hkv, causal):
+    """the 8-wave forward (scalar / packed FMA softmax) against the fp32 reference at D = 128 and GQA groups of 4, 1
+    and 2, with and without the O^T output (which must be the exact transpose of O)."""
+    from kubeoperator_amd.ops.reference import attention_ref
+
+    old = lib().flash_attn_set_fwd_variant(variant)
+    try:
+        D = 128
+        torch.manual_seed(B * S + Hq)
+        qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
+        a, c = Hq * D, (Hq + Hkv) * D
+        q, k, v = qkv[:, :a], qkv[:, a:c], qkv[:, c:]
+        o = torch.empty(B * S, Hq * D, device=DEV, dtype=torch.bfloat16)
+        lse = torch.empty(B * Hq * S, device=DEV)
+        lib().flash_attn_fwd(q, k, v, o, lse, B, S, Hq, Hkv, D, D ** -0.5, causal)
+        o_ref, lse_ref = attention_ref(q, k, v, B, S, Hq, Hkv, D, causal)
+        assert rel_err(o, o_ref) < 2e-2
+        assert (lse - lse_ref.reshape(lse.shape)).abs().max().item() < 2e-2
+        o1, ot = torch.empty_like(o), torch.empty(Hq * D, B * S, device=DEV, dtype=torch.bfloat16)
+        l1 = torch.empty_like(lse)
+        lib().flash_attn_fwd_t(q, k, v, o1, ot, l1, B, S, Hq, Hkv, D, D ** -0.5, causal)
+        assert torch.equal(o1, o) and torch.equal(l1, lse)
+        assert torch.equal(ot, o1.t())
+    finally:
+        lib().flash_attn_set_fwd_variant(old)
 
 
 @pytest.mark.parametrize("D,Hq,Hkv", [(128, 8, 2), (64, 4, 4)])

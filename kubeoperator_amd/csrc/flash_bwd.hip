@@ -339,119 +339,6 @@ __global__ void __launch_bounds__(NW * 64, (NW >= 8 ? 1 : 2)) fa_bwd_dkdv_kernel
   }
 }
 
-// dQ = scale * dS.K from the TRANSPOSED dS written by fa_bwd_dkdv64_kernel ([B, Hq, key, query]): the same
-// workgroup shape and K-tile ring as fa_bwd_dq_ds_kernel, but every wave stages its own [64 keys][32 queries]
-// dS^T block (64-B rows, four 1-KiB DMA pieces per tile: one wave instruction = 16 key rows) and reads its
-// B fragments with ds_read_b64_tr_b16 -- a half-wave's transposed read covers 4 whole 64-B rows = all 64
-// banks once, so the plain image is conflict-free.
-template <int D, int HP>
-__global__ void __launch_bounds__(512, 1) fa_bwd_dq_dst_kernel(const bf16_t* __restrict__ dst,
-                                                               const bf16_t* __restrict__ k, bf16_t* __restrict__ dq,
-                                                               int B, int S, int Hq, int Hkv, int64_t ks, int64_t dqs,
-                                                               float scale, int causal) {
-  constexpr int NW = 8, BM = 256, RH = BM / HP, WPH = NW / HP, BN = 64, ROWB = D * 2, NSLOT = 3;
-  constexpr int KT = BN * ROWB, WST = BN * 64, SLOT = KT + NW * WST;
-  constexpr int PPW = (KT / 1024) / NW + WST / 1024;  // DMA pieces per wave per tile
-  static_assert((KT / 1024) % NW == 0, "K tile must split evenly over the waves");
-  static_assert(RH % 32 == 0, "each wave owns 32 rows of one head");
-  constexpr int DT = D / 32, NR = 2 * DT, RB = ROWB * 8;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 31, hh = lane >> 5;
-  const int tq = (lane & 15) >> 2, tp = lane & 3, tg1 = (lane >> 4) & 1;
-  const int ngrp = Hq / HP, nqb = S / RH;
-  const AttnWork aw = attn_work(blockIdx.x, B, ngrp, (Hq / Hkv) / HP, nqb);
-  const int qb = causal ? (nqb - 1 - aw.rank) : aw.rank;
-  const int b = aw.b, hg = aw.unit;
-  const int kvh = (hg * HP) / (Hq / Hkv);
-  const int hq = hg * HP + wid / WPH;
-  const int q0 = qb * RH, q0w = q0 + 32 * (wid % WPH);
-  const int ntiles = causal ? (q0 + RH + BN - 1) / BN : S / BN;
-  const bf16_t* kbase = k + (int64_t)(b * S) * ks + kvh * D;
-  // this wave's dS^T block: key rows of its head, columns q0w .. q0w+31
-  const bf16_t* dsw = dst + ((int64_t)(b * Hq + hq) * S) * S + q0w;
-  auto issue = [&](int t) {
-    char* sl = smem + (t % NSLOT) * SLOT;
-    dma_tile_a<ROWB, NW, BN>(sl, kbase + (int64_t)(t * BN) * ks, ks, wid, lane);
-    char* wsl = sl + KT + wid * WST;
-#pragma unroll
-    for (int i = 0; i < WST / 1024; ++i) {
-      const int row = 16 * i + (lane >> 2);
-      glds16(dsw + (int64_t)(t * BN + row) * S + 8 * (lane & 3), wsl + 1024 * i);
-    }
-  };
-  issue(0);
-  if (ntiles > 1) issue(1);
-
-  // transposed reads: K^T (swizzled sub-tiled image, as fa_bwd_dq_ds_kernel) and dS^T (plain 64-B rows:
-  // rows R0 + 4hh + tq, columns 16tg1 + 4tp)
-  const int kb_lane0 = 64 * (4 * hh + tq) + 16 * ((2 * tg1 + (tp >> 1)) ^ hh) + 8 * (tp & 1);
-  const int kb_lane1 = 64 * (4 * hh + tq) + 16 * ((2 * tg1 + (tp >> 1)) ^ (2 + hh)) + 8 * (tp & 1);
-  const int ds_lane = 64 * (4 * hh + tq) + 2 * (16 * tg1 + 4 * tp);
-  f32x16 acc[DT];
-#pragma unroll
-  for (int i = 0; i < DT; ++i) acc[i] = f32x16{0};
-  const int qi = q0w + r;
-
-  for (int it = 0; it < ntiles; ++it) {
-    if (it + 1 < ntiles) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (it + 2 < ntiles) issue(it + 2);
-    const int kv0 = it * BN;
-    if (!causal || kv0 <= q0w + 31) {
-      const char* sl = smem + (it % NSLOT) * SLOT;
-      const uint32_t kb0 = lds_addr(sl) + kb_lane0, kb1 = lds_addr(sl) + kb_lane1;
-      const uint32_t db = lds_addr(sl + KT + wid * WST) + ds_lane;
-      const bool diag = causal && kv0 + BN - 1 > q0w;
-      static_for<4>([&](auto ks4c) {
-        constexpr int ks4 = decltype(ks4c)::value;
-        constexpr int R0 = 16 * ks4;
-        bf16x4 t[NR + 2];
-        static_for<DT>([&](auto dtc) {
-          constexpr int dt = decltype(dtc)::value;
-          t[2 * dt] = lds_tr_read_off<RB * (R0 >> 3) + 512 * dt>(((R0 >> 3) & 1) ? kb1 : kb0);
-          t[2 * dt + 1] = lds_tr_read_off<RB * ((R0 + 8) >> 3) + 512 * dt>((((R0 + 8) >> 3) & 1) ? kb1 : kb0);
-        });
-        t[NR] = lds_tr_read_off<64 * R0>(db);
-        t[NR + 1] = lds_tr_read_off<64 * (R0 + 8)>(db);
-        if constexpr (NR + 2 == 10) {
-          asm volatile("s_waitcnt lgkmcnt(0)"
-                       : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]), "+v"(t[6]),
-                         "+v"(t[7]), "+v"(t[8]), "+v"(t[9]));
-        } else {
-          asm volatile("s_waitcnt lgkmcnt(0)"
-                       : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]));
-        }
-        bf16x8 fb = cat44(t[NR], t[NR + 1]);
-        if (diag) {  // keys past the query: zero (fully masked 32x32 blocks were never written)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int key = kv0 + R0 + 4 * hh + (e & 3) + 8 * (e >> 2);
-            if (key > qi) fb[e] = 0;
-          }
-        }
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) acc[dt] = mfma32(cat44(t[2 * dt], t[2 * dt + 1]), fb, acc[dt]);
-      });
-    }
-    asm volatile("" ::: "memory");
-  }
-  bf16_t* dp = dq + (int64_t)(b * S + qi) * dqs + hq * D;
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) {
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      u32x2 w;
-      w[0] = pack2(acc[dt][4 * g4] * scale, acc[dt][4 * g4 + 1] * scale);
-      w[1] = pack2(acc[dt][4 * g4 + 2] * scale, acc[dt][4 * g4 + 3] * scale);
-      *reinterpret_cast<u32x2*>(dp + dt * 32 + 8 * g4 + 4 * hh) = w;
-    }
-  }
-}
-
 // =============================================================================================
 // dQ
 // =============================================================================================
@@ -1004,24 +891,12 @@ static void launch_dkdv_ds(const bf16_t* q, const bf16_t* k, const bf16_t* v, co
         q, k, v, dout, nlse, ndelta, dk_part, dv_part, ds, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);
 }
 
-template <int D, int HP>
-static void launch_dq_dst(const bf16_t* ds, const bf16_t* k, bf16_t* dq, int B, int S, int Hq, int Hkv, int64_t ks,
-                          int64_t dqs, float scale, bool causal, hipStream_t stream) {
-  const size_t lds = 3 * (64 * (D * 2) + 8 * 64 * 64);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)fa_bwd_dq_dst_kernel<D, HP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    attr = true;
-  }
-  fa_bwd_dq_dst_kernel<D, HP><<<B * (Hq / HP) * (S / (256 / HP)), 512, lds, stream>>>(ds, k, dq, B, S, Hq, Hkv, ks,
-                                                                                     dqs, scale, causal);
-}
-
 static int g_dkdv_cfg = -1;  // -1: read KOP_DKDV_CFG on first use
 static int dkdv_cfg() {
   if (g_dkdv_cfg < 0) {
-    const char* e = getenv("KOP_DKDV_CFG");  // 64: one wave per SIMD, 64 keys per wave (D = 128); 42, 83, 82
+    // 64: one wave per SIMD, 64 keys per wave, wave-block dS (D = 128); 66: the same with row-major dS; 42: two
+    // waves per SIMD (every D); 83 / 82: 8-wave workgroups with a 3- / 2-deep stage ring (D = 128)
+    const char* e = getenv("KOP_DKDV_CFG");
     g_dkdv_cfg = e ? atoi(e) : 64;
   }
   return g_dkdv_cfg;
@@ -1088,17 +963,6 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
           else if (hp == 2) launch_dq_ds<D, 2>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
           else launch_dq_ds<D, 1>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
         }
-        if (!direct) fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs);
-        return;
-      }
-      if (cfg == 65 && S % 256 == 0) {
-        // transposed dS (direct 16-B stores, half lines per stage): the dQ kernel that reads it
-        flash_attn_bwd_dkdv64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs,
-                              dos, dks, dvs, scale, cflag, false, false, stream);
-        if (hp == 8) launch_dq_dst<D, 8>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-        else if (hp == 4) launch_dq_dst<D, 4>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-        else if (hp == 2) launch_dq_dst<D, 2>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-        else launch_dq_dst<D, 1>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
         if (!direct) fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs);
         return;
       }

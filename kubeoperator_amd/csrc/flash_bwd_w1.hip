@@ -87,7 +87,8 @@ __device__ __forceinline__ void vm_wait_le(int n) {
 // (KOP_DKDV64_DIAG, wrong results): 2 no exponentials, 4 no stage DMA, 8 no stage barrier, 32 no DMA wait; 16
 // non-temporal dS stores (correct, slower).
 // QM: dS in the query-major layout of fa_bwd_dkdv_kernel ([B, Hq, query, slot(key)]), staged through LDS so each
-// wave writes whole 128-B lines (its 64 keys are one line of every query row); else transposed, stored directly.
+// wave writes whole 128-B lines (its 64 keys are one line of every query row). (QM = false, a transposed layout
+// stored straight from the accumulators, measured slower and is no longer launched: profiles/r3_experiments.md.)
 // BLK (with QM): wave-block dS layout [B, Hq, S/32, S/64, 32 queries, 64 slots]: a wave's stage tile is one contiguous
 // 4 KB block (its workgroup's stage: 16 KB), instead of 32 rows of 128 B spread 2*S bytes apart.
 template <int D, bool DIRECT, int NS, bool QM, int DIAG = 0, bool BLK = false>
@@ -480,13 +481,11 @@ void flash_attn_bwd_dkdv64(const bf16_t* q, const bf16_t* k, const bf16_t* v, co
     if (Hq == Hkv) KOP_LAUNCH(true, true, 1, false);
     else KOP_LAUNCH(false, true, 1, false);
   } else if (Hq == Hkv) {
-    if (qm && blk_layout) KOP_LAUNCH(true, true, 0, true);
-    else if (qm) KOP_LAUNCH(true, true, 0, false);
-    else KOP_LAUNCH(true, false, 0, false);
+    if (blk_layout) KOP_LAUNCH(true, true, 0, true);
+    else KOP_LAUNCH(true, true, 0, false);
   } else {
-    if (qm && blk_layout) KOP_LAUNCH(false, true, 0, true);
-    else if (qm) KOP_LAUNCH(false, true, 0, false);
-    else KOP_LAUNCH(false, false, 0, false);
+    if (blk_layout) KOP_LAUNCH(false, true, 0, true);
+    else KOP_LAUNCH(false, true, 0, false);
   }
 #undef KOP_LAUNCH
 }

@@ -91,7 +91,10 @@ __device__ __forceinline__ void vm_wait_le(int n) {
 // stored straight from the accumulators, measured slower and is no longer launched: profiles/r3_experiments.md.)
 // BLK (with QM): wave-block dS layout [B, Hq, S/32, S/64, 32 queries, 64 slots]: a wave's stage tile is one contiguous
 // 4 KB block (its workgroup's stage: 16 KB), instead of 32 rows of 128 B spread 2*S bytes apart.
-template <int D, bool DIRECT, int NS, bool QM, int DIAG = 0, bool BLK = false>
+// REV: sweep the query stages from the last one down to the workgroup's diagonal. Every workgroup of a head then
+// reads the same Q / dO stage at the same time (forward order starts workgroup kb 8*kb stages later, so a stage is
+// re-read ~16 us apart -- long enough for the dS write stream to evict it from the XCD's 4 MB L2).
+template <int D, bool DIRECT, int NS, bool QM, int DIAG = 0, bool BLK = false, bool REV = false>
 __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ nlse, const float* __restrict__ ndelta,
@@ -137,10 +140,14 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     }
   };
   dma_tile_a<ROWB, NW, BN>(Kl, k + (int64_t)(b * S + k0) * ks + kvh * D, ks, wid, lane);
-  issue(qt0);
+  // stage order: qt0, qt0 + 1, ... (forward) or nqt - 1, nqt - 2, ... (REV); nxt(qt, i) is i stages later
+  auto nxt = [&](int x, int i) { return REV ? x - i : x + i; };
+  auto valid = [&](int x) { return REV ? x >= qt0 : x < nqt; };
+  const int first = REV ? nqt - 1 : qt0;
+  issue(first);
 #pragma unroll
   for (int i = 1; i < NS - 1; ++i)
-    if (qt0 + i < nqt) issue(qt0 + i);
+    if (valid(nxt(first, i))) issue(nxt(first, i));
 
   const int rb_lane0 = RB * (r >> 3) + 64 * (r & 7) + 16 * (hh ^ ((r >> 2) & 3));
   const int rb_lane1 = RB * (r >> 3) + 64 * (r & 7) + 16 * ((2 + hh) ^ ((r >> 2) & 3));
@@ -189,14 +196,14 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     // DMA(qt) is older than: stores(qt-2), DMA(qt+NS-2), stores(qt-1) (and the other DMAs still in flight)
     int younger = st1 + st2;
 #pragma unroll
-    for (int i = 1; i < NS - 1; ++i) younger += (qt + i < nqt) ? pcount : 0;
+    for (int i = 1; i < NS - 1; ++i) younger += valid(nxt(qt, i)) ? pcount : 0;
     if constexpr (!(DIAG & 36)) vm_wait_le(younger);
     st2 = st1;
     st1 = 0;
     if constexpr (!(DIAG & 8)) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if constexpr (!(DIAG & 4)) {
-      if (qt + NS - 1 < nqt) issue(qt + NS - 1);
+      if (valid(nxt(qt, NS - 1))) issue(nxt(qt, NS - 1));
     }
     const int qs0 = qt * BQ;
     if (causal && qs0 + BQ - 1 < k0w) return;  // every query of the stage precedes every key of the wave
@@ -388,12 +395,16 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     }
     asm volatile("" ::: "memory");
   };
-  int qt = qt0;
-  if (causal) {
-    const int qd = qt0 + BN / BQ < nqt ? qt0 + BN / BQ : nqt;
+  // the causal mask is needed only in the first BN / BQ stages of the forward order
+  const int qd = causal ? (qt0 + BN / BQ < nqt ? qt0 + BN / BQ : nqt) : qt0;
+  if constexpr (REV) {
+    for (int qt = nqt - 1; qt >= qd; --qt) body(qt, std::false_type{});
+    for (int qt = qd - 1; qt >= qt0; --qt) body(qt, std::true_type{});
+  } else {
+    int qt = qt0;
     for (; qt < qd; ++qt) body(qt, std::true_type{});
+    for (; qt < nqt; ++qt) body(qt, std::false_type{});
   }
-  for (; qt < nqt; ++qt) body(qt, std::false_type{});
   // the accumulators leave the AGPRs through compiler v_accvgpr_read: 18 wait states after the last 16-pass MFMA
   // that wrote them (hipcc pads nothing after an asm MFMA)
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3"
@@ -449,22 +460,28 @@ void flash_attn_bwd_dkdv64(const bf16_t* q, const bf16_t* k, const bf16_t* v, co
     return e ? atoi(e) : 0;
   }();
   // one instantiation per (DIRECT, QM, DIAG) actually launched; the dynamic-LDS attribute is set on first use
-#define KOP_LAUNCH(DIR, QMV, DG, BL)                                                                                    \
+#define KOP_LAUNCH(DIR, QMV, DG, BL) KOP_LAUNCH_R(DIR, QMV, DG, BL, true)
+#define KOP_LAUNCH_FWD(DIR, QMV, DG, BL) KOP_LAUNCH_R(DIR, QMV, DG, BL, false)
+#define KOP_LAUNCH_R(DIR, QMV, DG, BL, RV)                                                                              \
   do {                                                                                                             \
     static bool attr = false;                                                                                      \
     if (!attr) {                                                                                                   \
-      (void)hipFuncSetAttribute((const void*)fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG, BL>,                              \
+      (void)hipFuncSetAttribute((const void*)fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG, BL, RV>,                              \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                             \
       attr = true;                                                                                                 \
     }                                                                                                              \
     if (DIR)                                                                                                       \
-      fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG, BL><<<grid, 256, lds, stream>>>(                                    \
+      fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG, BL, RV><<<grid, 256, lds, stream>>>(                                \
           q, k, v, dout, nlse, ndelta, reinterpret_cast<float*>(dk), reinterpret_cast<float*>(dv), ds, B, S, Hq, Hkv, \
           qs, ks, vs, dos, scale, causal, dks, dvs);                                                               \
     else                                                                                                           \
-      fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG, BL><<<grid, 256, lds, stream>>>(                                    \
+      fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG, BL, RV><<<grid, 256, lds, stream>>>(                                \
           q, k, v, dout, nlse, ndelta, dk_part, dv_part, ds, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal, 0, 0);  \
   } while (0)
+  static const bool rev = [] {
+    const char* e = getenv("KOP_DKDV_REV");  // reversed stage sweep (default on); 0: forward order
+    return e ? atoi(e) != 0 : true;
+  }();
   if (diag != 0 && Hq != Hkv && qm && ds != nullptr) {
     switch (diag) {
       case 1: KOP_LAUNCH(false, true, 1, false); return;
@@ -480,6 +497,9 @@ void flash_attn_bwd_dkdv64(const bf16_t* q, const bf16_t* k, const bf16_t* v, co
   if (ds == nullptr) {  // no dS at all (dQ recomputes it): the store-free build
     if (Hq == Hkv) KOP_LAUNCH(true, true, 1, false);
     else KOP_LAUNCH(false, true, 1, false);
+  } else if (!rev && Hq != Hkv) {  // forward stage order (A/B)
+    if (blk_layout) KOP_LAUNCH_FWD(false, true, 0, true);
+    else KOP_LAUNCH_FWD(false, true, 0, false);
   } else if (Hq == Hkv) {
     if (blk_layout) KOP_LAUNCH(true, true, 0, true);
     else KOP_LAUNCH(true, true, 0, false);
@@ -488,6 +508,8 @@ void flash_attn_bwd_dkdv64(const bf16_t* q, const bf16_t* k, const bf16_t* v, co
     else KOP_LAUNCH(false, true, 0, false);
   }
 #undef KOP_LAUNCH
+#undef KOP_LAUNCH_FWD
+#undef KOP_LAUNCH_R
 }
 
 }  // namespace kop

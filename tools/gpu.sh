@@ -27,7 +27,7 @@
 source "$(dirname "$0")/gpu_lib.sh"
 mkdir -p gpurun_out/prof gpurun_out/pmc
 
-L8B="python bench.py --steps 10 --warmup 3"
+L8B="${L8B:-python bench.py --steps 10 --warmup 3}"
 G2="python bench.py --model gpt2_small --seq 1024 --mbs 32 --steps 20 --warmup 5"
 port=29700
 

@@ -945,12 +945,22 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
     const int grp = Hq / Hkv;  // heads per dQ workgroup: largest power of two dividing the GQA group, <= 8
     const int hp = (grp % 8 == 0) ? 8 : (grp % 4 == 0) ? 4 : (grp % 2 == 0) ? 2 : 1;
     bool done = false;
+    if (D == 64 && cfg == 640 && S % 256 == 0) {  // one-wave dK/dV at D = 64 (opt-in)
+      flash_attn_bwd_dkdv64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, D, qs, ks, vs, dos,
+                            dks, dvs, scale, cflag, true, true, stream);
+      if (hp == 8) launch_dq_ds<D, 8, true>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+      else if (hp == 4) launch_dq_ds<D, 4, true>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+      else if (hp == 2) launch_dq_ds<D, 2, true>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+      else launch_dq_ds<D, 1, true>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+      if (!direct) fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs);
+      return;
+    }
     if constexpr (D == 128) {  // 8 waves need >= 8 1-KiB pieces per Q / dO tile (32 rows x 256 B)
       if ((cfg == 64 || cfg == 66) && S % 256 == 0) {
         // one wave per SIMD, query-major dS staged through LDS (whole-line stores) -- in the wave-block layout (64)
         // or plain rows (66) -- read by the materialised-dS dQ kernel
         const bool blk = cfg == 64;
-        flash_attn_bwd_dkdv64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs,
+        flash_attn_bwd_dkdv64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, D, qs, ks, vs,
                               dos, dks, dvs, scale, cflag, true, blk, stream);
         if (blk) {
           if (hp == 8) launch_dq_ds<D, 8, true>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
@@ -989,8 +999,8 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
   if (D == 128 && dkdv_cfg() == 64 && S % 256 == 0) {
     // the one-wave dK/dV kernel without dS stores; dQ recomputes S and dP below. It writes bf16 dK / dV itself
     // when Hq == Hkv, so the finalize pass is then skipped.
-    flash_attn_bwd_dkdv64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, nullptr, B, S, Hq, Hkv, qs, ks, vs,
-                          dos, dks, dvs, scale, causal ? 1 : 0, false, false, stream);
+    flash_attn_bwd_dkdv64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, nullptr, B, S, Hq, Hkv, D, qs, ks,
+                          vs, dos, dks, dvs, scale, causal ? 1 : 0, false, false, stream);
   } else {
     fa_bwd_dkdv_kernel<D, NW, false><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(
         q, k, v, dout, nlse, ndelta, dk_part, dv_part, nullptr, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);

@@ -294,10 +294,11 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
       }
       if constexpr (kk + 3 < NK) cur = dor(std::integral_constant<int, kk + 3>{});
       if constexpr (kk == NK - 3) trr(o0, o1, std::integral_constant<int, 0>{}, ta);
+      // this step's slice of the 16 scores per block: EP = 16 / NK elements (2 at D = 128, 4 at D = 64)
+      constexpr int EP = 16 / NK;
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        constexpr int j0 = 2 * kk;
-        const int j = j0 + e;
+      for (int e = 0; e < EP; ++e) {
+        const int j = EP * kk + e;
         float a = (DIAG & 2) ? s0[j] * c2 : __builtin_amdgcn_exp2f(s0[j] * c2);
         float c = (DIAG & 2) ? s1[j] * c2 : __builtin_amdgcn_exp2f(s1[j] * c2);
         if constexpr (MASK) {
@@ -307,8 +308,11 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
         s0[j] = a;
         s1[j] = c;
       }
-      pw0[kk >> 2][kk & 3] = pack2(s0[2 * kk], s0[2 * kk + 1]);
-      pw1[kk >> 2][kk & 3] = pack2(s1[2 * kk], s1[2 * kk + 1]);
+#pragma unroll
+      for (int pi = EP * kk / 2; pi < EP * (kk + 1) / 2; ++pi) {
+        pw0[pi >> 2][pi & 3] = pack2(s0[2 * pi], s0[2 * pi + 1]);
+        pw1[pi >> 2][pi & 3] = pack2(s1[2 * pi], s1[2 * pi + 1]);
+      }
       __builtin_amdgcn_sched_barrier(0);
     });
     const bf16x8 pb0[2] = {__builtin_bit_cast(bf16x8, pw0[0]), __builtin_bit_cast(bf16x8, pw0[1])};
@@ -337,42 +341,64 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
       }
       if constexpr (dt + 1 < DT) trr(o0, o1, std::integral_constant<int, dt + 1>{}, (dt & 1) ? ta : tb);
       else trr(qa0, qa1, std::integral_constant<int, 0>{}, (dt & 1) ? ta : tb);
+      // this step's slice of dS = p * (dP - delta): ED = 16 / DT elements (4 at D = 128, 8 at D = 64); query half
+      // hs (elements 8hs .. 8hs+7) is complete -- and stored -- at the step that finishes its element 8hs + 7
+      constexpr int ED = 16 / DT;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int j = 4 * dt + e;
+      for (int e = 0; e < ED; ++e) {
+        const int j = ED * dt + e;
         p0[j] *= s0[j];
         p1[j] *= s1[j];
       }
-      sw0[dt >> 1][2 * (dt & 1)] = pack2(p0[4 * dt], p0[4 * dt + 1]);
-      sw0[dt >> 1][2 * (dt & 1) + 1] = pack2(p0[4 * dt + 2], p0[4 * dt + 3]);
-      sw1[dt >> 1][2 * (dt & 1)] = pack2(p1[4 * dt], p1[4 * dt + 1]);
-      sw1[dt >> 1][2 * (dt & 1) + 1] = pack2(p1[4 * dt + 2], p1[4 * dt + 3]);
-      if constexpr ((dt & 1) && (DIAG & 1)) asm volatile("" ::"v"(sw0[dt >> 1]), "v"(sw1[dt >> 1]));
-      if constexpr ((dt & 1) && !(DIAG & 1)) {
-        if constexpr (QM) {
-          stage_w<(dt >> 1)>(sw0[dt >> 1], (dt >> 1) ? stw1 : stw0, std::integral_constant<int, 0>{});
-          stage_w<(dt >> 1)>(sw1[dt >> 1], (dt >> 1) ? stw1 : stw0, std::integral_constant<int, 2048>{});
-        } else {
-          st(sw0[dt >> 1], row0, dt >> 1, dsoff);
-          st(sw1[dt >> 1], row1, dt >> 1, dsoff);
-        }
+#pragma unroll
+      for (int pi = ED * dt / 2; pi < ED * (dt + 1) / 2; ++pi) {
+        sw0[pi >> 2][pi & 3] = pack2(p0[2 * pi], p0[2 * pi + 1]);
+        sw1[pi >> 2][pi & 3] = pack2(p1[2 * pi], p1[2 * pi + 1]);
       }
+      static_for<2>([&](auto hc) {
+        constexpr int hs = decltype(hc)::value;
+        constexpr bool done_here = (ED * (dt + 1) > 8 * hs + 7) && (ED * dt <= 8 * hs + 7);
+        if constexpr (done_here && (DIAG & 1)) asm volatile("" ::"v"(sw0[hs]), "v"(sw1[hs]));
+        if constexpr (done_here && !(DIAG & 1)) {
+          if constexpr (QM) {
+            stage_w<hs>(sw0[hs], hs ? stw1 : stw0, std::integral_constant<int, 0>{});
+            stage_w<hs>(sw1[hs], hs ? stw1 : stw0, std::integral_constant<int, 2048>{});
+          } else {
+            st(sw0[hs], row0, hs, dsoff);
+            st(sw1[hs], row1, hs, dsoff);
+          }
+        }
+      });
       __builtin_amdgcn_sched_barrier(0);
     });
     st1 = (DIAG & 1) ? 0 : 4;
     const bf16x8 sb0[2] = {__builtin_bit_cast(bf16x8, sw0[0]), __builtin_bit_cast(bf16x8, sw0[1])};
     const bf16x8 sb1[2] = {__builtin_bit_cast(bf16x8, sw1[0]), __builtin_bit_cast(bf16x8, sw1[1])};
-    // ---- dK^T += Q^T.dS (16 MFMAs); QM: the staged dS tile goes out as whole lines, one store per step
+    // ---- dK^T += Q^T.dS; QM: the staged dS tile goes out as whole lines in 4 store instructions, SPI = 4 / DT per
+    // step (each two transposed reads, stored one step later)
     const uint64_t dsq0 = BLK ? dsq + 4096ull * (uint64_t)qt * (uint64_t)(S / 64) : dsq + 2ull * (uint64_t)qs0 * (uint64_t)S;
-    bf16x4 xa[2], xb[2];
+    constexpr int SPI = 4 / DT;
+    static_assert(SPI * DT == 4 && (SPI == 1 || SPI == 2), "4 staged store instructions over the dK steps");
+    bf16x4 xa[2 * SPI], xb[2 * SPI];
+    auto xwait = [&](bf16x4* t, bf16x4* x) {
+      if constexpr (SPI == 1)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(x[0]), "+v"(x[1]));
+      else
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]));
+    };
     static_for<DT>([&](auto dtc) {
       constexpr int dt = decltype(dtc)::value;
       bf16x4* t = ((DT + dt) & 1) ? tb : ta;  // Q^T block 0 went to the buffer after the last dO^T block
       bf16x4* xc = (dt & 1) ? xb : xa;
       bf16x4* xp = (dt & 1) ? xa : xb;
       if constexpr (QM && !(DIAG & 1)) {
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(xp[0]), "+v"(xp[1]));
-        if constexpr (dt > 0) stage_st<dt - 1, (DIAG & 16) != 0>(xp, dsq0, sqoff);
+        xwait(t, xp);
+        if constexpr (dt > 0)
+          static_for<SPI>([&](auto uc) {
+            constexpr int u = decltype(uc)::value;
+            stage_st<(dt - 1) * SPI + u, (DIAG & 16) != 0>(xp + 2 * u, dsq0, sqoff);
+          });
       } else {
         wait_tr<4, 0>(t);
       }
@@ -382,16 +408,22 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
         mfma32_agpr(dk1[dt], cat44(t[2 * s], t[2 * s + 1]), sb1[s]);
       }
       if constexpr (dt + 1 < DT) trr(qa0, qa1, std::integral_constant<int, dt + 1>{}, ((DT + dt) & 1) ? ta : tb);
-      if constexpr (QM && !(DIAG & 1)) {
-        xc[0] = lds_tr_read_off<1024 * dt>(str);
-        xc[1] = lds_tr_read_off<1024 * dt + 512>(str);
-      }
+      if constexpr (QM && !(DIAG & 1))
+        static_for<SPI>([&](auto uc) {
+          constexpr int u = decltype(uc)::value, I = dt * SPI + u;
+          xc[2 * u] = lds_tr_read_off<1024 * I>(str);
+          xc[2 * u + 1] = lds_tr_read_off<1024 * I + 512>(str);
+        });
       __builtin_amdgcn_sched_barrier(0);
     });
     if constexpr (QM && !(DIAG & 1)) {
       bf16x4* xl = ((DT - 1) & 1) ? xb : xa;
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xl[0]), "+v"(xl[1]));
-      stage_st<DT - 1, (DIAG & 16) != 0>(xl, dsq0, sqoff);
+      if constexpr (SPI == 1) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xl[0]), "+v"(xl[1]));
+      else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(xl[0]), "+v"(xl[1]), "+v"(xl[2]), "+v"(xl[3]));
+      static_for<SPI>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        stage_st<(DT - 1) * SPI + u, (DIAG & 16) != 0>(xl + 2 * u, dsq0, sqoff);
+      });
     }
     asm volatile("" ::: "memory");
   };
@@ -448,11 +480,12 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
   out(dk1, dv1, k0w + 32 + r);
 }
 
-void flash_attn_bwd_dkdv64(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout, const float* nlse,
-                           const float* ndelta, float* dk_part, float* dv_part, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B,
-                           int S, int Hq, int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t dos, int64_t dks,
-                           int64_t dvs, float scale, int causal, bool qm, bool blk_layout, hipStream_t stream) {
-  constexpr int D = 128, NS = 3;
+template <int D>
+static void dkdv64_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout, const float* nlse,
+                          const float* ndelta, float* dk_part, float* dv_part, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B,
+                          int S, int Hq, int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t dos, int64_t dks,
+                          int64_t dvs, float scale, int causal, bool qm, bool blk_layout, hipStream_t stream) {
+  constexpr int NS = 3;
   const size_t lds = 256 * (D * 2) + NS * (2 * 32 * (D * 2) + 1024) + 4 * 4096;
   const dim3 grid(B * Hq * (S / 256));
   static const int diag = [] {
@@ -510,6 +543,18 @@ void flash_attn_bwd_dkdv64(const bf16_t* q, const bf16_t* k, const bf16_t* v, co
 #undef KOP_LAUNCH
 #undef KOP_LAUNCH_FWD
 #undef KOP_LAUNCH_R
+}
+
+void flash_attn_bwd_dkdv64(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout, const float* nlse,
+                           const float* ndelta, float* dk_part, float* dv_part, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B,
+                           int S, int Hq, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t dos, int64_t dks,
+                           int64_t dvs, float scale, int causal, bool qm, bool blk_layout, hipStream_t stream) {
+  if (D == 128)
+    dkdv64_launch<128>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs, dos, dks,
+                       dvs, scale, causal, qm, blk_layout, stream);
+  else
+    dkdv64_launch<64>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs, dos, dks,
+                      dvs, scale, causal, qm, blk_layout, stream);
 }
 
 }  // namespace kop

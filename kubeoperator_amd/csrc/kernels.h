@@ -79,12 +79,12 @@ int flash_attn_set_dkdv_cfg(int c);
 // forward kernel variant: -1 per-head-dim default, 8 / 9 / 10 the 8-wave kernel, < 8 the 4-wave kernel; returns the old
 // setting (an argument below -1 only reads it)
 int flash_attn_set_fwd_variant(int v);
-// one-wave-per-SIMD dK/dV kernel (flash_bwd_w1.hip), D = 128, S % 256 == 0. ds: the query-major dS that
+// one-wave-per-SIMD dK/dV kernel (flash_bwd_w1.hip), D = 128 or 64, S % 256 == 0. ds: the query-major dS that
 // fa_bwd_dq_ds_kernel reads (blk_layout: its wave-block form), or nullptr for the store-free build (dQ recomputed);
 // qm is kept for the call sites and must be true when ds is set
 void flash_attn_bwd_dkdv64(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout, const float* nlse,
                            const float* ndelta, float* dk_part, float* dv_part, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B,
-                           int S, int Hq, int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t dos, int64_t dks,
+                           int S, int Hq, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t dos, int64_t dks,
                            int64_t dvs, float scale, int causal, bool qm, bool blk_layout, hipStream_t stream);
 int flash_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
                    const float* lse, bf16_t* dq, bf16_t* dk, bf16_t* dv, void* workspace, int B, int S, int Hq,

@@ -333,14 +333,16 @@ def test_weight_grad_tn_layout_matches_nt(layout, monkeypatch):
         assert rel_err(out, 2 * ref) < 1e-2
 
 
-@pytest.mark.parametrize("variant,cfg", [(10, 64), (10, 66), (10, 42), (9, 64), (9, 42), (8, 42)],
-                         ids=["ds_blk-dkdv64", "ds-dkdv66", "ds-dkdv42", "recompute9-dkdv64", "recompute9", "recompute8"])
+@pytest.mark.parametrize("variant,cfg", [(10, 64), (10, 66), (10, 640), (10, 42), (9, 64), (9, 42), (8, 42)],
+                         ids=["ds_blk-dkdv64", "ds-dkdv66", "ds_blk-dkdv64_d64", "ds-dkdv42", "recompute9-dkdv64",
+                              "recompute9", "recompute8"])
 @pytest.mark.parametrize("D,Hq,Hkv,S", [(128, 8, 2, 512), (64, 4, 4, 256), (128, 4, 1, 768), (128, 8, 1, 256),
                                         (64, 8, 4, 512), (128, 4, 4, 512), (128, 6, 2, 512), (128, 2, 1, 256)])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_attention_bwd_dq_variants(variant, cfg, D, Hq, Hkv, S, causal):
     """every dQ algorithm (recompute 8/9, materialised dS 10) and dK/dV kernel (64 / 66: one wave per SIMD
-    with the wave-block / row query-major dS staged through LDS, D = 128; 42: two waves per SIMD) against the fp32 autograd reference. The shapes cover the
+    with the wave-block / row query-major dS staged through LDS, D = 128; 640: the same at D = 64; 42: two waves per
+    SIMD) against the fp32 autograd reference. The shapes cover the
     no-GQA direct path (Hq == Hkv) and every dQ head grouping (8, 4, 2, 1 heads per workgroup)."""
     from kubeoperator_amd.ops.functional import rope_attention
     from kubeoperator_amd.ops.reference import attention_ref

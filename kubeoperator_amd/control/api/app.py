@@ -42,6 +42,15 @@ API = "/api/v1"
 UI_DIR = os.path.join(os.path.dirname(os.path.dirname(__file__)), "ui")
 
 
+def _is_ipv4(v: str) -> bool:
+    import ipaddress
+
+    try:
+        return isinstance(ipaddress.ip_address(v), ipaddress.IPv4Address)
+    except ValueError:
+        return False
+
+
 class HTTPError(Exception):
     def __init__(self, status: int, detail: Any):
         self.status, self.detail = status, detail
@@ -881,6 +890,26 @@ def create_app() -> FastAPI:
         d = await body(request)
         context.set_settings(d, tab=request.query_params.get("tab", "system"))
         return context.get_settings(request.query_params.get("tab"))
+
+    # ------------------------------------------------------------------ DNS (ui/src/app/dns/dns.service.ts)
+    # Cluster-wide resolvers for the nodes: stored as the "dns" settings tab, so every execution's extra vars carry
+    # dns1 / dns2 to the nameserver role (a zone's own dns1 / dns2 override them: zone vars are applied later).
+    @r.get("/dns/")
+    def get_dns(request: Request):
+        current_user(request)
+        st = context.get_settings("dns")
+        return {"id": "dns", "dns1": st.get("dns1", ""), "dns2": st.get("dns2", "")}
+
+    @r.post("/dns/update/")
+    async def update_dns(request: Request):
+        superuser(request)
+        d = await body(request)
+        vals = {k: str(d.get(k) or "").strip() for k in ("dns1", "dns2")}
+        for k, v in vals.items():
+            if v and not _is_ipv4(v):
+                raise HTTPError(400, {k: [f"not an IPv4 address: {v!r}"]})
+        context.set_settings(vals, tab="dns")
+        return {"id": "dns", **vals}
 
     # ------------------------------------------------------------------ cloud provider (cloud_provider/api.py)
     @r.get("/provider/template/")

@@ -507,11 +507,25 @@ views.users = crudPage("Users", "/users/", [["Username", "username"], ["Email", 
   {extraButtons: `<button class="secondary" onclick="POST('/users/sync/').then(()=>alert('LDAP sync queued'))">Sync LDAP</button>`});
 
 views.settings = async (v, [tab = "system"]) => {
-  const tabs = ["system", "backup-storage", "ldap", "notification"];
+  const tabs = ["system", "dns", "backup-storage", "ldap", "notification"];
   v.innerHTML = `<h2>Settings</h2><div class="tabs">${tabs.map((t) => `<a href="#/settings/${t}" class="${t === tab ? "active" : ""}">${t}</a>`).join("")}</div><div id="tab"></div>`;
   const t = $("#tab");
   if (tab === "backup-storage") return crudPage("Backup storage", "/backupStorage/", [["Name", "name"], ["Type", "type"], ["Region", "region"], ["Status", (b) => st(b.status)]],
     [["name", "Name"], ["type", "Type", "select", ["S3", "OSS", "AZURE", "LOCAL"]], ["region", "Region"], ["credentials", "Credentials (JSON: bucket, accessKey, secretKey, endpoint | path)", "json"]])(t);
+  if (tab === "dns") {  // cluster-wide node resolvers (the reference's DNS page): /dns/, /dns/update/
+    const d = await GET("/dns/");
+    t.innerHTML = `<form id="df" class="card"><label>DNS1<input name="dns1" value="${esc(d.dns1)}"></label><label>DNS2<input name="dns2" value="${esc(d.dns2)}"></label>
+      <div class="toolbar"><button type="submit">Save</button></div><p id="df-msg" class="muted">Written to every node's resolv.conf at install; a zone's own dns1 / dns2 take precedence.</p></form>`;
+    $("#df").addEventListener("submit", async (e) => {
+      e.preventDefault();
+      const f = new FormData(e.target);
+      try {
+        await POST("/dns/update/", {dns1: f.get("dns1"), dns2: f.get("dns2")});
+        $("#df-msg").textContent = "Saved.";
+      } catch (err) { $("#df-msg").textContent = String(err.message || err); }
+    });
+    return;
+  }
   const keys = {system: ["local_hostname", "domain_suffix", "ntp_server", "REGISTRY_PREFIX"], ldap: ["AUTH_LDAP_ENABLE", "AUTH_LDAP_SERVER_URI", "AUTH_LDAP_BIND_DN", "AUTH_LDAP_BIND_PASSWORD", "AUTH_LDAP_SEARCH_OU", "AUTH_LDAP_SEARCH_FILTER", "AUTH_LDAP_USER_ATTR_MAP"],
     notification: ["SMTP_ADDRESS", "SMTP_PORT", "SMTP_USERNAME", "SMTP_PASSWORD", "SMTP_USE_SSL", "DINGTALK_WEBHOOK", "DINGTALK_SECRET", "WORKWEIXIN_CORP_ID", "WORKWEIXIN_AGENT_ID", "WORKWEIXIN_SECRET"]}[tab];
   const cur = await GET(`/settings?tab=${tab}`);

@@ -157,6 +157,14 @@ def test_crud_resources_and_secrets(client):
     st = client.get("/api/v1/settings", params={"tab": "system"}).json()
     assert st["local_hostname"] == "10.0.0.100" and st["SMTP_PASSWORD"] == ""
 
+    # DNS page (ui/src/app/dns): stored as the "dns" settings tab, carried to the nameserver role via extra vars
+    assert client.get("/api/v1/dns/").json() == {"id": "dns", "dns1": "", "dns2": ""}
+    assert client.post("/api/v1/dns/update/", json={"dns1": "10.0.0.53", "dns2": "not-an-ip"}).status_code == 400
+    assert client.post("/api/v1/dns/update/", json={"dns1": "10.0.0.53", "dns2": ""}).json()["dns1"] == "10.0.0.53"
+    assert client.get("/api/v1/dns/").json()["dns1"] == "10.0.0.53"
+    from kubeoperator_amd.control.domain import context as ctx
+    assert ctx.get_settings()["dns1"] == "10.0.0.53"  # clusters.extra_vars merges every settings tab
+
     pk = client.get("/api/v1/packages/").json()
     assert {"mi355x-k8s", "mi355x-k8s-next"} <= {p["name"] for p in pk}
     assert client.get("/api/v1/cluster/config").json()["templates"]

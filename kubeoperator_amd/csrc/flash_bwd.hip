@@ -891,6 +891,17 @@ static void launch_dkdv_ds(const bf16_t* q, const bf16_t* k, const bf16_t* v, co
         q, k, v, dout, nlse, ndelta, dk_part, dv_part, ds, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);
 }
 
+// dQ from the materialised dS with HP q-heads of a GQA group per workgroup (HP the largest power of two <= 8
+// dividing the group)
+template <int D, bool BLK>
+static void launch_dq_ds_hp(int hp, const bf16_t* ds, const bf16_t* k, bf16_t* dq, int B, int S, int Hq, int Hkv,
+                            int64_t ks, int64_t dqs, float scale, bool causal, hipStream_t stream) {
+  if (hp == 8) launch_dq_ds<D, 8, BLK>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+  else if (hp == 4) launch_dq_ds<D, 4, BLK>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+  else if (hp == 2) launch_dq_ds<D, 2, BLK>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+  else launch_dq_ds<D, 1, BLK>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+}
+
 static int g_dkdv_cfg = -1;  // -1: read KOP_DKDV_CFG on first use
 static int dkdv_cfg() {
   if (g_dkdv_cfg < 0) {
@@ -944,55 +955,33 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
     const int cflag = causal ? 1 : 0;
     const int grp = Hq / Hkv;  // heads per dQ workgroup: largest power of two dividing the GQA group, <= 8
     const int hp = (grp % 8 == 0) ? 8 : (grp % 4 == 0) ? 4 : (grp % 2 == 0) ? 2 : 1;
+    // one wave per SIMD (flash_bwd_w1.hip): query-major dS staged through LDS into whole-line stores, in the
+    // wave-block layout (cfg 64; 640 = the same at D = 64, opt-in) or plain rows (66)
+    const bool one_wave = S % 256 == 0 && ((D == 128 && (cfg == 64 || cfg == 66)) || (D == 64 && cfg == 640));
+    const bool blk = one_wave && cfg != 66;
     bool done = false;
-    if (D == 64 && cfg == 640 && S % 256 == 0) {  // one-wave dK/dV at D = 64 (opt-in)
+    if (one_wave) {
       flash_attn_bwd_dkdv64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, D, qs, ks, vs, dos,
-                            dks, dvs, scale, cflag, true, true, stream);
-      if (hp == 8) launch_dq_ds<D, 8, true>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-      else if (hp == 4) launch_dq_ds<D, 4, true>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-      else if (hp == 2) launch_dq_ds<D, 2, true>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-      else launch_dq_ds<D, 1, true>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-      if (!direct) fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs);
-      return;
+                            dks, dvs, scale, cflag, true, blk, stream);
+      done = true;
     }
-    if constexpr (D == 128) {  // 8 waves need >= 8 1-KiB pieces per Q / dO tile (32 rows x 256 B)
-      if ((cfg == 64 || cfg == 66) && S % 256 == 0) {
-        // one wave per SIMD, query-major dS staged through LDS (whole-line stores) -- in the wave-block layout (64)
-        // or plain rows (66) -- read by the materialised-dS dQ kernel
-        const bool blk = cfg == 64;
-        flash_attn_bwd_dkdv64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, D, qs, ks, vs,
-                              dos, dks, dvs, scale, cflag, true, blk, stream);
-        if (blk) {
-          if (hp == 8) launch_dq_ds<D, 8, true>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-          else if (hp == 4) launch_dq_ds<D, 4, true>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-          else if (hp == 2) launch_dq_ds<D, 2, true>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-          else launch_dq_ds<D, 1, true>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-        } else {
-          if (hp == 8) launch_dq_ds<D, 8>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-          else if (hp == 4) launch_dq_ds<D, 4>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-          else if (hp == 2) launch_dq_ds<D, 2>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-          else launch_dq_ds<D, 1>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-        }
-        if (!direct) fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs);
-        return;
-      }
-      if (cfg == 83 && S % 256 == 0) {
-        launch_dkdv_ds<D, 8, 3>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks,
-                                vs, dos, dks, dvs, scale, cflag, stream);
+    if constexpr (D == 128) {
+      // 8-wave workgroups (>= 8 1-KiB pieces per 32-row x 256-B Q / dO tile) with a 3- or 2-deep stage ring
+      if (!done && cfg == 83 && S % 256 == 0) {
+        launch_dkdv_ds<D, 8, 3>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs,
+                                dos, dks, dvs, scale, cflag, stream);
         done = true;
-      } else if (cfg == 82 && S % 256 == 0) {
-        launch_dkdv_ds<D, 8, 2>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks,
-                                vs, dos, dks, dvs, scale, cflag, stream);
+      } else if (!done && cfg == 82 && S % 256 == 0) {
+        launch_dkdv_ds<D, 8, 2>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs,
+                                dos, dks, dvs, scale, cflag, stream);
         done = true;
       }
     }
     if (!done)
       launch_dkdv_ds<D, NW, 2>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs,
                                dos, dks, dvs, scale, cflag, stream);
-    if (hp == 8) launch_dq_ds<D, 8>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-    else if (hp == 4) launch_dq_ds<D, 4>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-    else if (hp == 2) launch_dq_ds<D, 2>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-    else launch_dq_ds<D, 1>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+    if (blk) launch_dq_ds_hp<D, true>(hp, ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+    else launch_dq_ds_hp<D, false>(hp, ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
     if (!direct) fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs);
     return;
   }

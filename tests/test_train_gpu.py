@@ -223,3 +223,42 @@ def test_activation_recompute_matches_on_gpu(model):
     noise = (g0 - g1).norm().item() / scale
     diff = (g0 - g2).norm().item() / scale
     assert diff <= 4 * noise + 1e-3, (diff, noise)
+
+
+@pytest.mark.gpu
+def test_rccl_selftest_bench_one_rank():
+    """bench.py under torchrun with KOP_RCCL_SELFTEST=1 on the GPU: the process group is RCCL ("nccl" on ROCm) and
+    every data-parallel collective of the step -- ZeRO-1 reduce-scatter and all-gather, grad-norm all-reduce,
+    barriers -- runs through it, matching the plain one-rank step's loss."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = str(s.getsockname()[1])
+    args = ["--model", "tiny_llama", "--seq", "256", "--mbs", "2", "--accum", "2", "--steps", "2", "--warmup", "1",
+            "--bucket-mb", "1", "--gemm-tuning", "off"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+
+    def run(cmd, extra):
+        p = subprocess.run(cmd, cwd=root, env={**env, **extra}, capture_output=True, text=True, timeout=240)
+        assert p.returncode == 0, p.stderr[-3000:]
+        lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+        assert len(lines) == 1, p.stdout[-2000:]
+        return lines[0]
+
+    r = run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "1",
+             "--master-addr", "127.0.0.1", "--master-port", port, "bench.py", "--gpus", "1"] + args,
+            {"KOP_RCCL_SELFTEST": "1"})
+    assert r["backend"] == "nccl" and r["rccl_world"] == 1
+    assert r["config"]["parallelism"] == "dp1-zero1"
+    assert r["grad_comm_bytes_per_step"] > 0 and r["param_gather_bytes_per_step"] > 0
+    assert r["exposed_comm_ms"] is not None
+    plain = run([sys.executable, "bench.py", "--gpus", "1"] + args, {})
+    assert plain["backend"] == "none"
+    assert abs(plain["last_loss"] - r["last_loss"]) < 2e-2, (plain["last_loss"], r["last_loss"])

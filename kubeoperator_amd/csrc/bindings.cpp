@@ -42,6 +42,20 @@ const bf16_t* cbp(const c10::optional<Tensor>& t) {
 }
 void rc(int code, const char* what) { TORCH_CHECK(code == 0, what, " failed with code ", code, " (unsupported shape)"); }
 
+// ------------------------------------------------------------------ decode projections
+Tensor gemv(const Tensor& x, const Tensor& w) {
+  check_bf16(x, "x");
+  check_bf16(w, "weight");
+  check_rows(x, "x");
+  check_rows(w, "weight");
+  const int M = (int)x.size(0), K = (int)x.size(1), N = (int)w.size(0);
+  TORCH_CHECK(w.size(1) == K, "gemv: x and weight disagree on K");
+  auto y = at::empty({M, N}, x.options());
+  rc(kop::gemv_bf16(bp(x), bp(w), bp(y), M, N, K, x.stride(0), w.stride(0), y.stride(0), cur_stream()),
+     "gemv (M <= 8, K a multiple of 1024)");
+  return y;
+}
+
 // ------------------------------------------------------------------ norms
 std::vector<Tensor> norm_fwd(const Tensor& x, const c10::optional<Tensor>& residual, const Tensor& w,
                              const c10::optional<Tensor>& b, double eps, bool layernorm) {
@@ -517,6 +531,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flash_attn_fwd_t", &flash_attn_fwd_t);
   m.def("decode_attn", &decode_attn);
   m.def("decode_rope_append_", &decode_rope_append_);
+  m.def("gemv", &gemv);
   m.def("flash_attn_bwd_workspace", &flash_attn_bwd_workspace);
   m.def("flash_attn_bwd", &flash_attn_bwd);
   m.def("flash_attn_set_dq_variant", [](int64_t v) { return (int64_t)kop::flash_attn_set_dq_variant((int)v); });

@@ -94,6 +94,9 @@ int flash_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16
 // decode_attn.hip: one query token per sequence against a [B, Hkv, Smax, D] KV cache (lens[b] valid keys),
 // split-K over 256-key chunks; part_o: B * Hq * nsplit * D floats, part_ml: B * Hq * nsplit * 2 floats
 int decode_attn_splits(int max_len);
+// gemv.hip: y[M, N] = x[M, K] . W[N, K]^T for M <= 8 decode rows (K a multiple of 1024); 1 = unsupported shape
+int gemv_bf16(const bf16_t* x, const bf16_t* w, bf16_t* y, int M, int N, int K, int64_t xs, int64_t ws, int64_t ys,
+              hipStream_t stream);
 // RoPE at pos[b] on the Q and K heads of each fused QKV row (in place) + K / V rows appended to the caches at pos[b]
 int decode_rope_append(bf16_t* qkv, int64_t qs, const float* cos_t, const float* sin_t, const int* pos, bf16_t* kc,
                        bf16_t* vc, int B, int Smax, int Hq, int Hkv, int D, hipStream_t stream);

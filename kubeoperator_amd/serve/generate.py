@@ -14,6 +14,7 @@ generator adds no autograd state (``torch.no_grad``). On CPU every op falls back
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -72,6 +73,8 @@ class LlamaGenerator:
         self.scale = 1.0 / math.sqrt(c.head_dim)
         self.graph = graph and self.device.type == "cuda"
         self._graphs: dict = {}  # batch -> (graph, static token input, static logits output)
+        # decode projections of <= GEMV_ROWS token rows through the HIP GEMV (csrc/gemv.hip); KOP_DECODE_GEMV=0: GEMMs
+        self._gemv = self.device.type == "cuda" and os.environ.get("KOP_DECODE_GEMV", "1") != "0"
 
     def drop_fp8(self) -> None:
         for blk in self.model.layers:
@@ -83,7 +86,27 @@ class LlamaGenerator:
     def _head(self):
         return self.model.tok_emb if self.cfg.tie_embeddings else self.model.lm_head
 
+    # rows routed to the GEMV: Llama-3-8B decode at batch 1 runs 4.35 vs 4.77 ms per step (+9.6 %), but at
+    # batch 4 / 8 the library GEMM is 15-20 % faster (profiles/r3_decode_gemv_ab.jsonl); the kernel takes up to 8
+    GEMV_ROWS = 1
+
+    def _gemv_ok(self, x, w) -> bool:
+        return (self._gemv and x.shape[0] <= self.GEMV_ROWS and x.shape[-1] % 1024 == 0
+                and w.dtype == torch.bfloat16 and not hasattr(w, "w8"))
+
+    def _lin(self, x, w):
+        """x . w^T: a decode step reads every weight once, so for a few token rows the HIP GEMV (weight rows
+        streamed at HBM rate) replaces the library GEMM's small-M tiles; FP8 weights and larger batches keep
+        ``kf.linear``."""
+        if self._gemv_ok(x, w):
+            from ..ops import load
+
+            return load().gemv(x, w)
+        return kf.linear(x, w)
+
     def _mlp(self, blk, y2):
+        if self._gemv_ok(y2, blk.w_gate_up) and self._gemv_ok(y2, blk.w_down):
+            return self._lin(kf.swiglu(self._lin(y2, blk.w_gate_up)), blk.w_down)
         return kf.swiglu_mlp(y2, blk.w_gate_up, blk.w_down)
 
     @torch.no_grad()
@@ -133,7 +156,7 @@ class LlamaGenerator:
                 o, _ = kf.flash_attention(q, k, v, B, S, Hq, Hkv, D, causal=True, scale=self.scale)
             else:
                 o, _ = ref.attention_ref(q, k, v, B, S, Hq, Hkv, D, True, self.scale)
-            y2, x = kf.rms_norm(x1, blk.mlp_norm, c.norm_eps, residual=kf.linear(o, blk.wo))
+            y2, x = kf.rms_norm(x1, blk.mlp_norm, c.norm_eps, residual=self._lin(o, blk.wo))
             pending = self._mlp(blk, y2)
         y, _ = kf.rms_norm(x, m.final_norm, c.norm_eps, residual=pending)
         lt = torch.tensor(lengths, dtype=torch.int32)
@@ -201,7 +224,7 @@ class LlamaGenerator:
                 y, x1 = kf.rms_norm(x, blk.attn_norm, c.norm_eps), x
             else:
                 y, x1 = kf.rms_norm(x, blk.attn_norm, c.norm_eps, residual=pending)
-            qkv = kf.linear(y, blk.wqkv)
+            qkv = self._lin(y, blk.wqkv)
             if qkv.is_cuda:  # one kernel: RoPE at pos on Q / K + K / V rows appended to the cache
                 from ..ops import load
 
@@ -211,11 +234,12 @@ class LlamaGenerator:
                 self.cache.k[i][rows, :, pl] = qkv[:, a:kc].reshape(B, Hkv, D)
                 self.cache.v[i][rows, :, pl] = qkv[:, kc:].reshape(B, Hkv, D)
             o = kf.decode_attention(qkv[:, :a], self.cache.k[i][:B], self.cache.v[i][:B], lens, max_len, self.scale)
-            y2, x = kf.rms_norm(x1, blk.mlp_norm, c.norm_eps, residual=kf.linear(o, blk.wo))
+            y2, x = kf.rms_norm(x1, blk.mlp_norm, c.norm_eps, residual=self._lin(o, blk.wo))
             pending = self._mlp(blk, y2)
         y, _ = kf.rms_norm(x, m.final_norm, c.norm_eps, residual=pending)
         self.cache.lens[:B] = lens if active is None else pos + active
-        return torch.mm(y, self._head().t()).float()
+        return self._lin(y, self._head()).float() if self._gemv_ok(y, self._head()) else \
+            torch.mm(y, self._head().t()).float()
 
     def _rows(self, B: int) -> torch.Tensor:
         key = ("rows", B)

@@ -36,11 +36,12 @@ import os
 import signal
 import subprocess
 import sys
+import threading
 import time
 
 import yaml
 
-SERVICES = ("web", "worker", "beat")
+SERVICES = ("web", "worker", "beat", "repo")  # repo: per-package file repository + OCI registry
 
 
 # ------------------------------------------------------------------------------------------------ bootstrap
@@ -108,6 +109,21 @@ def run_services(cfg, services: list[str]) -> int:
         pool = jobs.WorkerPool().start()
     if "beat" in services:
         sched = scheduler.Scheduler().start()
+    repo_stop = threading.Event()
+    if "repo" in services:  # reference: one Nexus container per package (package_manage.py:31-45)
+        from .domain import packages
+
+        host = str(cfg["HTTP_BIND_HOST"] or "0.0.0.0")
+        packages.serve_all(host)
+
+        def rescan():  # packages dropped into PACKAGE_DIR later are served without a restart
+            while not repo_stop.wait(60):
+                try:
+                    packages.serve_all(host)
+                except Exception:  # noqa: BLE001 -- a bad package must not stop the loop
+                    logging.getLogger("kubeops.packages").exception("package rescan failed")
+
+        threading.Thread(target=rescan, name="pkg-rescan", daemon=True).start()
     try:
         if "web" in services:
             from .api import create_app
@@ -122,6 +138,11 @@ def run_services(cfg, services: list[str]) -> int:
     except KeyboardInterrupt:
         pass
     finally:
+        repo_stop.set()
+        if "repo" in services:
+            from .domain import packages
+
+            packages.stop_servers()
         if pool:
             pool.stop()
         if sched:

@@ -4,9 +4,11 @@ Reference: kubeops_api/models/host.py:17-159 (gather_info :96-142, GPU via ``lsp
 :122-131), utils/gpu.py:4-9, serializers/host.py:28-43 (IP unique + SSH ping), host_import.py:12-63
 (xlsx import), models/health/host_health.py:9-42.
 
-GPU detection is AMD-first: ``lspci -nn -d 1002:`` lines of PCI class 0380/0300/0302 are matched
-against the AMD Instinct device-ID table (MI355X = 1002:75a3 ...), and ``amd-smi static --asic --vram``
-/ ``rocm-smi --showproductname`` output, when ROCm is already installed, refines product name and VRAM.
+GPU detection is AMD-first and needs no extra tool on the node: ``lspci -nn -d 1002:`` when pciutils is
+there, else ``/sys/bus/pci/devices/*/{vendor,class,device}``; PCI class 0380/0300/0302/1200 rows are matched
+against the AMD Instinct device-ID table (MI355X = 1002:75a3 ...). The kfd topology
+(``/sys/class/kfd/kfd/topology/nodes/*/properties``) supplies the architecture the ROCm runtime will report
+(``gfx_target_version`` 90500 -> gfx950), the CU count and VRAM; ``amd-smi list`` adds GPU indices / UUIDs.
 """
 from __future__ import annotations
 
@@ -77,16 +79,104 @@ def parse_amd_smi_list(text: str) -> list[dict]:
     return out
 
 
-GPU_PROBE = "lspci -nn -d 1002: 2>/dev/null; echo '--amd-smi--'; (amd-smi list 2>/dev/null || true)"
+# One shell round trip, four sections. lspci and amd-smi are optional tools; the two sysfs sections are always
+# there on a Linux host with the amdgpu driver bound, so a node without pciutils is still discovered.
+#   --sysfs--  one line per PCI function of vendor 0x1002: "<bdf> <class> <device> <numa_node>"
+#   --kfd--    one line per kfd topology node: "node <id> <key> <value> ..." (the node's properties file)
+GPU_PROBE = (
+    "(lspci -nn -d 1002: 2>/dev/null || true); echo '--amd-smi--'; (amd-smi list 2>/dev/null || true); "
+    "echo '--sysfs--'; for d in /sys/bus/pci/devices/*; do "
+    "[ \"$(cat $d/vendor 2>/dev/null)\" = 0x1002 ] && "
+    "echo \"${d##*/} $(cat $d/class) $(cat $d/device) $(cat $d/numa_node 2>/dev/null || echo -1)\"; done; "
+    "echo '--kfd--'; for n in /sys/class/kfd/kfd/topology/nodes/*; do "
+    "[ -f $n/properties ] && echo \"node ${n##*/} $(tr '\\n' ' ' < $n/properties)\"; done; true")
+
+GPU_CLASSES = ("0380", "0300", "0302", "1200")  # display / 3D / processing accelerator; skips audio, PSP, bridges
+
+
+def parse_sysfs_pci(text: str) -> list[dict]:
+    """Accelerators from the ``--sysfs--`` section: ``<bdf> 0x<class24> 0x<device> <numa>`` per AMD function."""
+    gpus = []
+    for line in text.splitlines():
+        parts = line.split()
+        if len(parts) < 3 or not parts[1].startswith("0x"):
+            continue
+        bdf, cls, dev = parts[0], parts[1][2:].rjust(6, "0")[:4].lower(), parts[2].lower().replace("0x", "")
+        if cls not in GPU_CLASSES:
+            continue
+        name, arch, vram = AMD_INSTINCT.get(dev, (f"AMD GPU [1002:{dev}]", "", 0))
+        g = {"name": name, "vendor": "amd", "pci": bdf, "device_id": f"1002:{dev}", "arch": arch, "vram_gb": vram}
+        if len(parts) > 3 and parts[3].lstrip("-").isdigit() and int(parts[3]) >= 0:
+            g["numa_node"] = int(parts[3])
+        gpus.append(g)
+    return gpus
+
+
+def gfx_name(target_version: int) -> str:
+    """kfd ``gfx_target_version`` (major*10000 + minor*100 + stepping) -> ``gfx950`` / ``gfx942`` / ``gfx90a``."""
+    major, minor, step = target_version // 10000, (target_version // 100) % 100, target_version % 100
+    return f"gfx{major}{minor:x}{step:x}"
+
+
+def parse_kfd_topology(text: str) -> list[dict]:
+    """GPU agents from the ``--kfd--`` section (CPU nodes have gfx_target_version 0)."""
+    out = []
+    for line in text.splitlines():
+        parts = line.split()
+        if len(parts) < 2 or parts[0] != "node":
+            continue
+        props = {}
+        for k, v in zip(parts[2::2], parts[3::2]):
+            try:
+                props[k] = int(v)
+            except ValueError:
+                continue
+        tv = props.get("gfx_target_version", 0)
+        if not tv:
+            continue
+        loc, dom = props.get("location_id", 0), props.get("domain", 0)
+        out.append({"node": int(parts[1]), "arch": gfx_name(tv), "vendor_id": props.get("vendor_id", 0),
+                    "device_id": f"{props.get('vendor_id', 0):04x}:{props.get('device_id', 0):04x}",
+                    "pci": f"{dom:04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 0x7}",
+                    "simd_count": props.get("simd_count", 0), "cu_count": props.get("simd_count", 0) // 4,
+                    "vram_bytes": props.get("local_mem_size", 0)})
+    return out
+
+
+def _same_bdf(a: str, b: str) -> bool:
+    """``05:00.0`` (lspci, no domain) matches ``0000:05:00.0`` (sysfs / amd-smi)."""
+    a, b = a.lower(), b.lower()
+    return a == b or a.endswith(b) or b.endswith(a)
 
 
 def detect_gpus(probe_stdout: str) -> list[dict]:
-    lspci, _, smi = probe_stdout.partition("--amd-smi--")
+    """Merge the probe's sections: lspci rows if pciutils is installed, else sysfs rows; then amd-smi indices /
+    UUIDs and the kfd topology's architecture (authoritative: it is what the ROCm runtime will report)."""
+    lspci, _, rest = probe_stdout.partition("--amd-smi--")
+    smi, _, rest = rest.partition("--sysfs--")
+    sysfs, _, kfd = rest.partition("--kfd--")
     gpus = parse_lspci_amd(lspci)
-    smi_rows = parse_amd_smi_list(smi)
+    sys_rows = parse_sysfs_pci(sysfs)
+    if not gpus:
+        gpus = sys_rows
+    else:
+        for g in gpus:  # full BDF and NUMA node from sysfs
+            for r in sys_rows:
+                if _same_bdf(r["pci"], g["pci"]):
+                    g["pci"] = r["pci"]
+                    if "numa_node" in r:
+                        g["numa_node"] = r["numa_node"]
+    agents = parse_kfd_topology(kfd)
     for g in gpus:
-        for row in smi_rows:
-            if row.get("bdf", "").endswith(g["pci"]):
+        for a in agents:
+            if _same_bdf(a["pci"], g["pci"]):
+                g["arch"] = a["arch"]
+                g["kfd_node"] = a["node"]
+                g["cu_count"] = a["cu_count"]
+                if not g.get("vram_gb") and a["vram_bytes"]:
+                    g["vram_gb"] = round(a["vram_bytes"] / 2 ** 30)
+        for row in parse_amd_smi_list(smi):
+            if _same_bdf(row.get("bdf", ""), g["pci"]):
                 g["index"] = row["gpu"]
                 g["uuid"] = row.get("uuid", "")
     return gpus
@@ -175,6 +265,31 @@ def gather_info(host_id: str, retry: int = 1) -> dict:
         h.gpus = gpus
         h.gpu_vendor = "amd" if gpus else ""
     return host_dict(host_id)
+
+
+def check_gpu_node(host_id: str, gpu_num: int | None = None) -> dict:
+    """Read-only GPU check on a registered host: the ``gpu-check`` tagged tasks of ``amdgpu-driver`` (kfd count)
+    and ``rocm-runtime`` (rocminfo agents, amd-smi inventory) through the engine -- no package tasks run.
+    Returns the engine summary plus the registered outputs."""
+    import os
+
+    from .plan import PLAYBOOK_DIR
+
+    with session_scope() as s:
+        h = s.get(M.Host, host_id)
+        n = gpu_num if gpu_num is not None else len(h.gpus or []) or 1
+    inv = _conn_inventory(h)
+    inv.add_group("gpu_nodes", {"gpu_num": n})
+    inv.add_host(h.name, groups=["gpu_nodes"])
+    cb = ResultCallback()
+    r = Runner(inv, context.transport(), forks=1, callback=cb, tags=["gpu-check"])
+    res = r.run_playbook(os.path.join(PLAYBOOK_DIR, "gpu-check.yml"))
+    ok = res["raw"]["ok"].get(h.name, {})
+    out = lambda name: next((str(v.get("stdout", "")).strip() for k, v in ok.items()  # noqa: E731
+                             if k.split(" : ")[-1] == name), "")
+    return {"summary": res["summary"], "kfd_gpus": out("count bound Instinct devices"),
+            "rocminfo_gpus": out("rocminfo sees every GPU agent"), "amd_smi": out("record GPU inventory"),
+            "tasks": sorted(ok)}
 
 
 def host_dict(host_id: str) -> dict:

@@ -17,9 +17,20 @@ import time
 
 from .transport import CmdResult, FakeTransport
 
+MI355X_BUSES = (0x05, 0x15, 0x65, 0x75, 0x85, 0x95, 0xe5, 0xf5)
 MI355X_LSPCI = "\n".join(
     f"{b:02x}:00.0 Processing accelerators [1200]: Advanced Micro Devices, Inc. [AMD/ATI] Device [1002:75a3]"
-    for b in (0x05, 0x15, 0x65, 0x75, 0x85, 0x95, 0xe5, 0xf5))
+    for b in MI355X_BUSES)
+# the probe's sysfs sections as a node with 8 MI355X shows them (hosts.GPU_PROBE): PCI functions of vendor
+# 0x1002 (the GPUs plus a non-GPU function that must be skipped) and the kfd topology (2 CPU nodes, 8 GPUs)
+MI355X_SYSFS = "\n".join(
+    [f"0000:{b:02x}:00.0 0x120000 0x75a3 {0 if i < 4 else 1}" for i, b in enumerate(MI355X_BUSES)]
+    + ["0000:04:00.0 0x060400 0x14a0 0"])
+MI355X_KFD = "\n".join(
+    ["node 0 cpu_cores_count 64 simd_count 0 gfx_target_version 0 vendor_id 0 device_id 0 location_id 0 domain 0",
+     "node 1 cpu_cores_count 64 simd_count 0 gfx_target_version 0 vendor_id 0 device_id 0 location_id 0 domain 0"]
+    + [f"node {2 + i} cpu_cores_count 0 simd_count 1024 gfx_target_version 90500 vendor_id 4098 device_id 30115 "
+       f"location_id {b << 8} domain 0 local_mem_size {288 * 2 ** 30}" for i, b in enumerate(MI355X_BUSES)])
 KUBECONFIG = """apiVersion: v1
 kind: Config
 clusters:
@@ -48,6 +59,7 @@ class SimFarm(FakeTransport):
         self.gpu_hosts = set(gpu_hosts or ())  # inventory names or addresses of the GPU machines
         self._addr: dict[str, str] = getattr(self, "_addr", {})
         self.gpus_per_host = gpus_per_host
+        self.no_pciutils: set = set()  # hosts whose probe has no lspci section (pciutils not installed)
         self._install_rules()
 
     BASE_FILES = {
@@ -151,7 +163,10 @@ class SimFarm(FakeTransport):
             return (0, data.decode(), "") if data else (1, "", "No such file")
 
         def gpu_probe(host, cmd, fs):
-            return 0, (MI355X_LSPCI + "\n--amd-smi--\n") if self.is_gpu(host) else "--amd-smi--\n", ""
+            if not self.is_gpu(host):
+                return 0, "--amd-smi--\n--sysfs--\n--kfd--\n" + MI355X_KFD.split("\n")[0] + "\n", ""
+            lspci = "" if host in self.no_pciutils else MI355X_LSPCI + "\n"
+            return 0, lspci + "--amd-smi--\n--sysfs--\n" + MI355X_SYSFS + "\n--kfd--\n" + MI355X_KFD + "\n", ""
 
         def snapshot_zip(host, cmd, fs):
             fs["/opt/kubeoperator/backup/cluster-backup.zip"] = b"PK\x05\x06" + b"\x00" * 18

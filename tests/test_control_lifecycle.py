@@ -47,6 +47,46 @@ def test_lspci_parsing():
     assert names == ["AMD Instinct MI355X", "AMD Instinct MI300X"]
 
 
+def test_gpu_discovery_without_pciutils_uses_sysfs_and_kfd(control):
+    """No lspci on the node: the sysfs PCI scan finds the GPUs, the kfd topology names the architecture."""
+    control.farm.no_pciutils.add("w1")
+    h = hosts.create_host({"name": "w1", "ip": "10.0.0.2", "password": "pw"})
+    assert h["gpu_num"] == 8 and h["gpu_info"] == "AMD Instinct MI355X"
+    g = h["gpus"][0]
+    assert g["pci"] == "0000:05:00.0" and g["device_id"] == "1002:75a3" and g["arch"] == "gfx950"
+    assert g["cu_count"] == 256 and g["numa_node"] == 0 and h["gpus"][-1]["numa_node"] == 1
+    assert all(x["pci"] != "0000:04:00.0" for x in h["gpus"])  # the AMD bridge function is not a GPU
+
+
+def test_kfd_topology_parsing():
+    text = "\n".join([
+        "node 0 cpu_cores_count 96 simd_count 0 gfx_target_version 0 location_id 0 domain 0",
+        "node 1 cpu_cores_count 0 simd_count 1024 gfx_target_version 90500 vendor_id 4098 device_id 30115 "
+        "location_id 1280 domain 0 local_mem_size 309237645312",
+        "node 2 simd_count 440 gfx_target_version 90010 vendor_id 4098 device_id 29711 location_id 49417 domain 1"])
+    agents = hosts.parse_kfd_topology(text)
+    assert [a["arch"] for a in agents] == ["gfx950", "gfx90a"]
+    assert agents[0]["pci"] == "0000:05:00.0" and agents[0]["device_id"] == "1002:75a3"
+    assert agents[1]["pci"] == "0001:c1:01.1"
+    assert hosts.gfx_name(90402) == "gfx942"
+
+
+def test_unknown_device_id_takes_arch_from_kfd():
+    probe = ("--amd-smi--\n--sysfs--\n0000:05:00.0 0x120000 0x75b0 0\n--kfd--\n"
+             "node 1 simd_count 1024 gfx_target_version 90500 vendor_id 4098 device_id 30128 location_id 1280 domain 0")
+    (g,) = hosts.detect_gpus(probe)
+    assert g["arch"] == "gfx950" and g["device_id"] == "1002:75b0" and "75b0" in g["name"]
+
+
+def test_gpu_node_check_runs_only_read_only_tasks(control):
+    h = hosts.create_host({"name": "w1", "ip": "10.0.0.2", "password": "pw"})
+    r = hosts.check_gpu_node(h["id"])
+    assert r["summary"]["success"], r
+    assert r["kfd_gpus"] == "8" and r["rocminfo_gpus"] == "8", r["tasks"]
+    cmds = control.farm.commands("w1")
+    assert not any(c.startswith(("apt-get", "dnf", "modprobe", "udevadm")) or "amdgpu-dkms" in c for c in cmds)
+
+
 def test_full_lifecycle(control):
     _cluster()
     e = deploy.create("demo", "install", run="inline")

@@ -1,0 +1,229 @@
+"""Offline package endpoints: the repo service serves each package's file repository on
+``repo_port`` and a read-only OCI distribution registry on ``registry_port``; clashing ports are refused and
+the install preflight fails when the endpoints cannot be reached.
+
+Reference: core/apps/kubeops_api/models/package.py:41-62 (a Nexus container per package at scan time),
+core/apps/kubeops_api/package_manage.py:31-45 (repo 8081 / docker registry ports).
+Requests below are the ones containerd's resolver and fetcher issue for ``<registry>/<name>:<tag>``.
+"""
+import hashlib
+import json
+import os
+import socket
+import urllib.error
+import urllib.request
+
+import pytest
+import yaml
+
+from kubeoperator_amd.control.domain import packages
+from kubeoperator_amd.control.domain.repo_server import DOCKER_MANIFEST, OCI_INDEX, OCI_MANIFEST
+
+# containerd's Accept header for a manifest resolve (remotes/docker/resolver.go)
+CONTAINERD_ACCEPT = ", ".join([DOCKER_MANIFEST, "application/vnd.docker.distribution.manifest.list.v2+json",
+                               OCI_MANIFEST, OCI_INDEX, "*/*"])
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _blob(root, data: bytes) -> dict:
+    d = hashlib.sha256(data).hexdigest()
+    os.makedirs(os.path.join(root, "blobs", "sha256"), exist_ok=True)
+    with open(os.path.join(root, "blobs", "sha256", d), "wb") as f:
+        f.write(data)
+    return {"digest": "sha256:" + d, "size": len(data)}
+
+
+def _manifest(root, mtype, arch):
+    cfg = _blob(root, json.dumps({"architecture": arch, "os": "linux", "rootfs": {"type": "layers"}}).encode())
+    layer = _blob(root, os.urandom(3000) + arch.encode())
+    cfg_type = ("application/vnd.docker.container.image.v1+json" if mtype == DOCKER_MANIFEST
+                else "application/vnd.oci.image.config.v1+json")
+    layer_type = ("application/vnd.docker.image.rootfs.diff.tar.gzip" if mtype == DOCKER_MANIFEST
+                  else "application/vnd.oci.image.layer.v1.tar+gzip")
+    body = json.dumps({"schemaVersion": 2, "mediaType": mtype, "config": {"mediaType": cfg_type, **cfg},
+                       "layers": [{"mediaType": layer_type, **layer}]}).encode()
+    return {"mediaType": mtype, **_blob(root, body)}, cfg, layer
+
+
+def make_package(base, name, repo_port, registry_port):
+    """A package dir with a tiny OCI layout (a two-arch index and a schema2 image) and a repo tree."""
+    root = os.path.join(base, name)
+    reg = os.path.join(root, "registry")
+    os.makedirs(reg)
+    amd64, cfg, layer = _manifest(reg, OCI_MANIFEST, "amd64")
+    arm64, _, _ = _manifest(reg, OCI_MANIFEST, "arm64")
+    index = json.dumps({"schemaVersion": 2, "mediaType": OCI_INDEX, "manifests": [
+        {**arm64, "platform": {"os": "linux", "architecture": "arm64"}},
+        {**amd64, "platform": {"os": "linux", "architecture": "amd64"}}]}).encode()
+    idx = {"mediaType": OCI_INDEX, **_blob(reg, index)}
+    pause, _, _ = _manifest(reg, DOCKER_MANIFEST, "amd64")
+    with open(os.path.join(reg, "oci-layout"), "w") as f:
+        f.write('{"imageLayoutVersion": "1.0.0"}')
+    with open(os.path.join(reg, "index.json"), "w") as f:
+        json.dump({"schemaVersion": 2, "manifests": [
+            {**idx, "annotations": {"org.opencontainers.image.ref.name": "flannel/flannel:v0.25.6"}},
+            {**pause, "annotations": {"io.containerd.image.name": "registry.k8s.io/kubernetes/pause:3.9",
+                                      "org.opencontainers.image.ref.name": "3.9"}},
+            {**pause, "annotations": {"org.opencontainers.image.ref.name": "latest"}},  # no name: not served
+        ]}, f)
+    os.makedirs(os.path.join(root, "repo", "apt", "22.04"))
+    os.makedirs(os.path.join(root, "repo", "binaries"))
+    with open(os.path.join(root, "repo", "apt", "22.04", "Packages"), "w") as f:
+        f.write("Package: amdgpu-dkms\nVersion: 1:6.14.14\n")
+    with open(os.path.join(root, "repo", "binaries", "helm-v3.15.4"), "wb") as f:
+        f.write(b"\x7fELF-helm")
+    with open(os.path.join(root, "meta.yml"), "w") as f:
+        yaml.safe_dump({"name": name, "version": "v1", "resource": "k8s",
+                        "vars": {"repo_port": repo_port, "registry_port": registry_port}}, f)
+    return {"index": idx, "amd64": amd64, "arm64": arm64, "pause": pause, "config": cfg, "layer": layer, "root": root}
+
+
+def _get(url, method="GET", headers=None, data=None):
+    req = urllib.request.Request(url, method=method, headers=headers or {}, data=data)
+    try:
+        with urllib.request.urlopen(req, timeout=10) as r:
+            return r.status, dict(r.headers), r.read()
+    except urllib.error.HTTPError as e:
+        return e.code, dict(e.headers), e.read()
+
+
+@pytest.fixture
+def served(control, tmp_path):
+    base = tmp_path / "packages"
+    base.mkdir()
+    control.cfg["PACKAGE_DIR"] = str(base)
+    rp, gp = _free_port(), _free_port()
+    pkg = make_package(str(base), "offline-a", rp, gp)
+    out = packages.serve_all("127.0.0.1")
+    try:
+        yield pkg, rp, gp, out, base
+    finally:
+        packages.stop_servers()
+
+
+def test_registry_serves_a_pull_like_containerd(served):
+    pkg, rp, gp, out, _ = served
+    assert out["offline-a"] == {"repo": rp, "registry": gp}
+    reg = f"http://127.0.0.1:{gp}"
+    st, h, body = _get(reg + "/v2/")
+    assert st == 200 and h["Docker-Distribution-API-Version"] == "registry/2.0"
+    # resolve: HEAD the tag, then GET by the digest the registry named
+    st, h, body = _get(reg + "/v2/flannel/flannel/manifests/v0.25.6", "HEAD", {"Accept": CONTAINERD_ACCEPT})
+    assert st == 200 and body == b""
+    assert h["Docker-Content-Digest"] == pkg["index"]["digest"] and h["Content-Type"] == OCI_INDEX
+    assert int(h["Content-Length"]) == pkg["index"]["size"]
+    st, h, body = _get(reg + f"/v2/flannel/flannel/manifests/{pkg['index']['digest']}", headers={"Accept": CONTAINERD_ACCEPT})
+    assert st == 200 and "sha256:" + hashlib.sha256(body).hexdigest() == pkg["index"]["digest"]
+    child = [m for m in json.loads(body)["manifests"] if m["platform"]["architecture"] == "amd64"][0]
+    st, h, body = _get(reg + f"/v2/flannel/flannel/manifests/{child['digest']}", headers={"Accept": CONTAINERD_ACCEPT})
+    assert st == 200 and h["Content-Type"] == OCI_MANIFEST and h["Docker-Content-Digest"] == child["digest"]
+    assert "sha256:" + hashlib.sha256(body).hexdigest() == child["digest"]
+    man = json.loads(body)
+    for d in [man["config"], *man["layers"]]:
+        st, h, blob = _get(reg + f"/v2/flannel/flannel/blobs/{d['digest']}")
+        assert st == 200 and h["Docker-Content-Digest"] == d["digest"] and len(blob) == d["size"]
+        assert "sha256:" + hashlib.sha256(blob).hexdigest() == d["digest"]
+    # a resumed layer download (Range)
+    layer = pkg["layer"]
+    st, h, part = _get(reg + f"/v2/flannel/flannel/blobs/{layer['digest']}", headers={"Range": "bytes=100-"})
+    assert st == 206 and h["Content-Range"] == f"bytes 100-{layer['size'] - 1}/{layer['size']}"
+    assert len(part) == layer["size"] - 100
+    st, h, _ = _get(reg + f"/v2/flannel/flannel/blobs/{layer['digest']}", "HEAD")
+    assert st == 200 and int(h["Content-Length"]) == layer["size"]
+
+
+def test_registry_accept_negotiation_and_names(served):
+    pkg, _, gp, _, _ = served
+    reg = f"http://127.0.0.1:{gp}"
+    # a client that only takes single-image OCI manifests gets the linux/amd64 child of the index
+    st, h, body = _get(reg + "/v2/flannel/flannel/manifests/v0.25.6", headers={"Accept": OCI_MANIFEST})
+    assert st == 200 and h["Docker-Content-Digest"] == pkg["amd64"]["digest"] and h["Content-Type"] == OCI_MANIFEST
+    # Docker schema2 image named by io.containerd.image.name (registry host stripped)
+    st, h, body = _get(reg + "/v2/kubernetes/pause/manifests/3.9", headers={"Accept": DOCKER_MANIFEST})
+    assert st == 200 and h["Content-Type"] == DOCKER_MANIFEST and h["Docker-Content-Digest"] == pkg["pause"]["digest"]
+    st, _, body = _get(reg + "/v2/kubernetes/pause/manifests/3.9", headers={"Accept": OCI_INDEX})
+    assert st == 404 and json.loads(body)["errors"][0]["code"] == "MANIFEST_UNKNOWN"
+    st, _, body = _get(reg + "/v2/_catalog")
+    assert json.loads(body)["repositories"] == ["flannel/flannel", "kubernetes/pause"]
+    st, _, body = _get(reg + "/v2/flannel/flannel/tags/list")
+    assert json.loads(body) == {"name": "flannel/flannel", "tags": ["v0.25.6"]}
+    for path, code, err in [("/v2/flannel/flannel/manifests/v9", 404, "MANIFEST_UNKNOWN"),
+                            ("/v2/nope/manifests/v1", 404, "NAME_UNKNOWN"),
+                            (f"/v2/kubernetes/pause/manifests/{pkg['amd64']['digest']}", 404, "MANIFEST_UNKNOWN"),
+                            ("/v2/flannel/flannel/blobs/sha256:" + "0" * 64, 404, "BLOB_UNKNOWN"),
+                            ("/v2/flannel/flannel/blobs/md5:abc", 400, "DIGEST_INVALID")]:
+        st, _, body = _get(reg + path)
+        assert st == code and json.loads(body)["errors"][0]["code"] == err, path
+    st, _, body = _get(reg + "/v2/flannel/flannel/blobs/uploads/", "POST", data=b"")
+    assert st == 405 and json.loads(body)["errors"][0]["code"] == "UNSUPPORTED"
+
+
+def test_registry_refuses_a_corrupt_blob(served):
+    pkg, _, gp, _, _ = served
+    p = os.path.join(pkg["root"], "registry", "blobs", "sha256", pkg["layer"]["digest"].split(":")[1])
+    with open(p, "r+b") as f:
+        f.write(b"X")
+    st, _, body = _get(f"http://127.0.0.1:{gp}/v2/flannel/flannel/blobs/{pkg['layer']['digest']}")
+    assert st == 404 and json.loads(body)["errors"][0]["code"] == "BLOB_UNKNOWN"
+
+
+def test_repo_serves_files_and_health(served):
+    pkg, rp, _, _, _ = served
+    st, _, body = _get(f"http://127.0.0.1:{rp}/repository/binaries/helm-v3.15.4")
+    assert st == 200 and body == b"\x7fELF-helm"
+    st, _, body = _get(f"http://127.0.0.1:{rp}/repository/apt/22.04/Packages")
+    assert st == 200 and b"amdgpu-dkms" in body
+    assert _get(f"http://127.0.0.1:{rp}/healthz")[0] == 200
+    assert _get(f"http://127.0.0.1:{rp}/meta.yml")[0] == 404  # only /repository/ is exposed
+    assert _get(f"http://127.0.0.1:{rp}/repository/../meta.yml")[0] == 404
+
+
+def test_package_list_reports_endpoints_and_new_packages_are_served(served):
+    pkg, rp, gp, _, base = served
+    rows = {r["name"]: r for r in packages.sync_packages()}
+    assert rows["offline-a"]["serving"] == {"repo": True, "registry": True} and not rows["offline-a"]["conflict"]
+    # a package dropped in later is served on the next scan (reference: Package.lookup at list time)
+    rp2, gp2 = _free_port(), _free_port()
+    make_package(str(base), "offline-b", rp2, gp2)
+    rows = {r["name"]: r for r in packages.sync_packages()}
+    assert rows["offline-b"]["serving"] == {"repo": True, "registry": True}
+    assert _get(f"http://127.0.0.1:{gp2}/v2/")[0] == 200
+
+
+def test_port_clash_is_refused(served):
+    pkg, rp, gp, _, base = served
+    make_package(str(base), "offline-z", _free_port(), gp)  # registry port of offline-a
+    rows = {r["name"]: r for r in packages.sync_packages()}
+    assert "already claimed by package offline-a" in rows["offline-z"]["conflict"]
+    assert rows["offline-z"]["serving"] == {"repo": False, "registry": False}
+    with pytest.raises(ValueError, match="not served"):
+        packages.serve_package("offline-z")
+
+
+def test_builtin_packages_do_not_clash(control):
+    rows = packages.sync_packages()
+    assert {r["name"] for r in rows} >= {"mi355x-k8s", "mi355x-k8s-next"}
+    assert not any(r["conflict"] for r in rows), [(r["name"], r["conflict"]) for r in rows]
+
+
+def test_install_preflight_checks_the_package_endpoints(control):
+    from kubeoperator_amd.control.domain import clusters, deploy, hosts
+
+    for hn, ip in (("m1", "10.0.0.1"), ("w1", "10.0.0.2")):
+        hosts.create_host({"name": hn, "ip": ip, "password": "pw"})
+    clusters.create_cluster({"name": "pf", "template": "single-master", "network_plugin": "flannel",
+                             "persistent_storage": "local-volume"})
+    clusters.add_node("pf", {"name": "m1", "host": "m1", "roles": ["master"]})
+    clusters.add_node("pf", {"name": "w1", "host": "w1", "roles": ["worker"]})
+    control.farm.add_rule(r"/healthz", rc=7, stderr="curl: (7) Failed to connect")
+    e = deploy.create("pf", "install", run="inline")
+    assert e["state"] == "FAILURE"
+    assert [s["status"] for s in e["steps"]][:2] == ["error", "pending"]
+    dark = json.dumps(e["result_summary"]["dark"])
+    assert "offline package repository and registry are reachable" in dark
+    assert not any(c.startswith("apt-get") for c in control.farm.commands("w1"))

@@ -432,6 +432,42 @@ def m_wait_for(ctx: ModuleContext, a: dict) -> dict:
     return out
 
 
+BOOT_ID = "cat /proc/sys/kernel/random/boot_id"
+
+
+def m_reboot(ctx: ModuleContext, a: dict) -> dict:
+    """Reboot the host and wait until it is back (Ansible ``reboot``): the boot id before, a detached
+    ``systemctl reboot`` (so the command returns before the connection drops), then the boot id polled until
+    it changes or ``reboot_timeout`` runs out; an unreachable host while it restarts is expected."""
+    from .transport import Unreachable
+
+    timeout = float(a.get("reboot_timeout", 600))
+    fake = isinstance(ctx.transport, FakeTransport)
+    poll = 0.0 if fake else float(a.get("poll_interval", 5))
+    t0 = time.time()
+    before = ctx.run(BOOT_ID).stdout.strip()
+    cmd = str(a.get("reboot_command", "systemctl reboot"))
+    ctx.run(f"nohup sh -c 'sleep 2; {cmd}' >/dev/null 2>&1 &")
+    if not fake:
+        time.sleep(float(a.get("pre_reboot_delay", 0)) + 5)
+    tries = 0
+    while time.time() - t0 < timeout and (not fake or tries < 50):
+        tries += 1
+        try:
+            r = ctx.run(BOOT_ID, timeout=30)
+        except (Unreachable, OSError, TimeoutError):
+            time.sleep(poll)
+            continue
+        now = r.stdout.strip()
+        if r.rc == 0 and now and now != before:
+            if not fake:
+                time.sleep(float(a.get("post_reboot_delay", 0)))
+            return {"changed": True, "rebooted": True, "elapsed": round(time.time() - t0, 1)}
+        time.sleep(poll)
+    return {"changed": True, "failed": True, "rebooted": False,
+            "msg": f"host did not come back within {timeout:.0f} s (boot id unchanged)"}
+
+
 _FACTS_PROBE = r"""
 echo "hostname=$(hostname -s 2>/dev/null || hostname)"
 echo "fqdn=$(hostname -f 2>/dev/null || hostname)"
@@ -536,7 +572,7 @@ MODULES = {
     "get_url": m_get_url, "synchronize": m_synchronize,
     "service": m_service, "systemd": m_service, "package": m_package, "yum": m_package, "apt": m_package,
     "dnf": m_package, "modprobe": m_modprobe, "sysctl": m_sysctl, "hostname": m_hostname,
-    "authorized_key": m_authorized_key, "wait_for": m_wait_for, "setup": m_setup, "gather_facts": m_setup,
+    "authorized_key": m_authorized_key, "wait_for": m_wait_for, "reboot": m_reboot, "setup": m_setup, "gather_facts": m_setup,
     "set_fact": m_set_fact, "debug": m_debug, "fail": m_fail, "assert": m_assert, "include_vars": m_include_vars,
     "meta": m_meta, "pause": m_pause, "ping": lambda ctx, a: {"changed": False, "ping": "pong"},
 }

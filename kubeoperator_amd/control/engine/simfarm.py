@@ -60,6 +60,10 @@ class SimFarm(FakeTransport):
         self._addr: dict[str, str] = getattr(self, "_addr", {})
         self.gpus_per_host = gpus_per_host
         self.no_pciutils: set = set()  # hosts whose probe has no lspci section (pciutils not installed)
+        # AMD GPU stack per host: installed amdgpu-dkms / ROCm versions (None: not installed), amdgpu module
+        # holders (a non-zero count makes the upgrade reboot instead of reloading) and the boot counter
+        self.gpu_stack: dict[str, dict] = {}
+        self.amdgpu_holders = 0
         self._install_rules()
 
     BASE_FILES = {
@@ -168,6 +172,41 @@ class SimFarm(FakeTransport):
             lspci = "" if host in self.no_pciutils else MI355X_LSPCI + "\n"
             return 0, lspci + "--amd-smi--\n--sysfs--\n" + MI355X_SYSFS + "\n--kfd--\n" + MI355X_KFD + "\n", ""
 
+        def stack(host):
+            with self._lock:
+                return self.gpu_stack.setdefault(host, {"dkms": None, "rocm": None, "boot": 0})
+
+        def pkg_install(host, cmd, fs):  # record pinned GPU packages, then fall through to success
+            import re as _re
+
+            st = stack(host)
+            m = _re.search(r"amdgpu-dkms[=-]([0-9][0-9.]*[0-9])", cmd)
+            if m:
+                st["dkms"] = m.group(1)
+            m = _re.search(r"rocm-core[=-]([0-9][0-9.]*[0-9])", cmd)
+            if m:
+                st["rocm"] = m.group(1) + (".0" if m.group(1).count(".") == 1 else "")
+            return 0, "", ""
+
+        def dkms_version(host, cmd, fs):  # the probe pipes dpkg-query's "1:6.14.14.30200000-2204" through sed
+            v = stack(host)["dkms"]
+            if "sed" in cmd:
+                return 0, v or "none", ""
+            return (0, f"1:{v}.30200000-2204", "") if v else (1, "", "no packages found matching amdgpu-dkms")
+
+        def rocm_version(host, cmd, fs):
+            v = stack(host)["rocm"]
+            if "sed" in cmd:
+                return 0, v or "none", ""
+            return (0, f"{v}-17", "") if v else (1, "", "No such file")
+
+        def reboot(host, cmd, fs):
+            stack(host)["boot"] += 1
+            return 0, "", ""
+
+        def boot_id(host, cmd, fs):
+            return 0, f"00000000-0000-4000-8000-{stack(host)['boot']:012d}", ""
+
         def snapshot_zip(host, cmd, fs):
             fs["/opt/kubeoperator/backup/cluster-backup.zip"] = b"PK\x05\x06" + b"\x00" * 18
             return 0, "", ""
@@ -241,6 +280,16 @@ class SimFarm(FakeTransport):
         R(r"^helm status \S+ -n \S+ -o json", stdout="deployed")
         R(r"kubectl -n \S+ logs -l app.kubernetes.io/instance=", fn=train_log)
         R(r"systemctl is-active", rc=3)
+        R(r"apt-get install .*(amdgpu-dkms|rocm-core)[=-]", fn=pkg_install)
+        R(r"dpkg-query -W -f='\$\{Version\}' amdgpu-dkms", fn=dkms_version)
+        R(r"^d=\$\( \(dpkg-query", fn=lambda h, c, fs: (
+            (0, f"{stack(h)['dkms']} {stack(h)['rocm']}", "") if stack(h)["dkms"] else (1, "", "not installed")))
+        R(r"cat /opt/rocm/\.info/version", fn=rocm_version)
+        R(r"awk '\$1 == \"amdgpu\" \{print \$3\}' /proc/modules", fn=lambda h, c, fs: (0, str(self.amdgpu_holders), ""))
+        R(r"nohup sh -c 'sleep 2; systemctl reboot'", fn=reboot)
+        R(r"^cat /proc/sys/kernel/random/boot_id$", fn=boot_id)
+        R(r"get node \S+ -o jsonpath='\{\.status\.allocatable\.amd", stdout="8")
+        R(r"get pod rocminfo-upgrade-\S+ -o jsonpath='\{\.status\.phase\}'", stdout="Succeeded")
 
     def is_sim(self) -> bool:
         return True

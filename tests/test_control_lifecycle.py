@@ -87,6 +87,82 @@ def test_gpu_node_check_runs_only_read_only_tasks(control):
     assert not any(c.startswith(("apt-get", "dnf", "modprobe", "udevadm")) or "amdgpu-dkms" in c for c in cmds)
 
 
+def _upgrade_slice(farm, op):
+    start = len(farm.log)
+    e = op()
+    return e, farm.log[start:]
+
+
+def _first(log, host, pattern):
+    for i, (h, c) in enumerate(log):
+        if h == host and re.search(pattern, c):
+            return i
+    raise AssertionError(f"no {pattern!r} on {host}")
+
+
+def test_upgrade_moves_the_gpu_pool_to_the_package_versions(control):
+    """drain -> device plugin off -> pinned install -> reload -> kfd / rocminfo -> plugin back
+    -> validation pod -> uncordon, on the GPU worker only; a no-op for the GPU stack when versions are equal."""
+    _cluster()
+    farm = control.farm
+    assert deploy.create("demo", "install", run="inline")["state"] == "SUCCESS"
+    assert farm.gpu_stack["w1"] == {"dkms": "6.14.14", "rocm": "7.0.0", "boot": 0}
+    assert "m1" not in farm.gpu_stack  # the control node never gets the GPU stack
+
+    # same package: the Kubernetes part runs, the GPU stack is left alone
+    e, log = _upgrade_slice(farm, lambda: deploy.create("demo", "upgrade", {"package": "mi355x-k8s"}, run="inline"))
+    assert e["state"] == "SUCCESS", e["result_summary"].get("dark")
+    gpu_ops = r"amdgpu-dkms[=-]|rocm-core[=-]|modprobe -r amdgpu|systemctl reboot|kubeoperator\.io/gpu-|rocminfo-w1"
+    assert not [c for _, c in log if re.search(gpu_ops, c)]
+    assert any(h == "m1" and "kubectl uncordon w1" in c for h, c in log)
+
+    # ROCm 7.0 -> 7.1, amdgpu-dkms 6.14 -> 6.16
+    e, log = _upgrade_slice(farm, lambda: deploy.create("demo", "upgrade", {"package": "mi355x-k8s-next"},
+                                                        run="inline"))
+    assert e["state"] == "SUCCESS", e["result_summary"].get("dark")
+    assert farm.gpu_stack["w1"]["dkms"] == "6.16.6" and farm.gpu_stack["w1"]["rocm"] == "7.1.0"
+    order = [
+        _first(log, "w1", r"/repository/rocm/apt/7\.1|sources\.list\.d|apt-get update"),  # repository re-run
+        _first(log, "m1", r"kubectl drain w1"),
+        _first(log, "m1", r"kubectl label node w1 kubeoperator\.io/gpu-$"),
+        _first(log, "m1", r"amdgpu-dp-ds --field-selector spec\.nodeName=w1"),
+        _first(log, "w1", r"amdgpu-dkms=6\.16\.6"),
+        _first(log, "w1", r"modprobe -r amdgpu && modprobe amdgpu"),
+        _first(log, "w1", r"kfd/topology/nodes/\*/gpu_id"),
+        _first(log, "w1", r"rocminfo \| awk"),
+        _first(log, "m1", r"kubectl label node w1 kubeoperator\.io/gpu=true"),
+        _first(log, "m1", r"kubectl apply -f /opt/kubeoperator/manifests/rocminfo-w1\.yaml"),
+        _first(log, "m1", r"get pod rocminfo-upgrade-w1"),
+        _first(log, "m1", r"kubectl uncordon w1"),
+    ]
+    assert order == sorted(order), order
+    assert not any(re.search(r"systemctl reboot", c) for _, c in log)  # no holders: reload, not reboot
+    # masters: no GPU-stack commands at all
+    assert not [c for h, c in log if h == "m1" and re.search(r"amdgpu-dkms|rocm-core|modprobe .*amdgpu", c)]
+    # the node's apt sources now name the new ROCm and driver repositories
+    src = farm.fs["w1"]["/etc/apt/sources.list.d/kubeoperator.list"].decode()
+    assert "/rocm/apt/7.1 " in src and "/amdgpu/apt/7.1.70100-1 " in src
+
+    # running it again is a no-op for the GPU stack
+    e, log = _upgrade_slice(farm, lambda: deploy.create("demo", "upgrade", {"package": "mi355x-k8s-next"},
+                                                        run="inline"))
+    assert e["state"] == "SUCCESS" and not [c for _, c in log if re.search(gpu_ops, c)]
+
+
+def test_gpu_upgrade_reboots_when_the_module_is_held(control):
+    _cluster()
+    farm = control.farm
+    assert deploy.create("demo", "install", run="inline")["state"] == "SUCCESS"
+    farm.amdgpu_holders = 3
+    e, log = _upgrade_slice(farm, lambda: deploy.create("demo", "upgrade", {"package": "mi355x-k8s-next"},
+                                                        run="inline"))
+    assert e["state"] == "SUCCESS", e["result_summary"].get("dark")
+    assert farm.gpu_stack["w1"]["boot"] == 1
+    assert not any("modprobe -r amdgpu" in c for _, c in log)
+    assert _first(log, "w1", r"systemctl reboot") < _first(log, "w1", r"kfd/topology/nodes/\*/gpu_id") \
+        < _first(log, "m1", r"kubectl uncordon w1")
+
+
 def test_full_lifecycle(control):
     _cluster()
     e = deploy.create("demo", "install", run="inline")

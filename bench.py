@@ -21,6 +21,9 @@ Communication evidence in the JSON (N > 1): ``backend``, ``rccl_world`` (``dist.
 reduce-scatter or all-reduce / the ZeRO-1 all-gather per optimizer step) and ``exposed_comm_ms`` (per step, max
 over ranks): the compute stream's stall between backward's last kernel and the completion of the last gradient
 collective, plus its stalls on ZeRO-1 all-gather gates in the next forward -- CUDA-event timed on the GPU.
+``runtime`` records torch / HIP / RCCL versions and every ``NCCL_*`` / ``RCCL_*`` / ``HSA_*`` / ``TORCH_NCCL_*`` /
+``HIP_*`` variable in effect; ``cpu_affinity_rank0`` the CPUs rank 0 was pinned to (N > 1: each rank is bound to
+its GPU's NUMA-local CPUs, ``parallel/dist.py`` ``bind_rank_cpus``).
 """
 from __future__ import annotations
 
@@ -112,11 +115,13 @@ def main() -> int:
 
     import torch
 
-    from kubeoperator_amd.parallel.dist import all_reduce_max, barrier, collectives_on, init_distributed, shutdown
+    from kubeoperator_amd.parallel.dist import (all_reduce_max, barrier, bind_rank_cpus, collectives_on,
+                                                init_distributed, runtime_env, shutdown)
     from kubeoperator_amd.models import get_config
     from kubeoperator_amd.train import SyntheticTokens, TrainConfig, Trainer
 
     info = init_distributed(args.device, timeout_s=args.comm_timeout)
+    affinity = bind_rank_cpus(info)  # multi-rank GPU jobs: each rank on the CPUs of its GPU's NUMA node
     if args.dp == "auto":
         args.dp = "zero1" if collectives_on(info) else "allreduce"
     from kubeoperator_amd.train import gemm_tuning
@@ -227,8 +232,13 @@ def main() -> int:
             "grad_comm_bytes_per_step": int(comm_step),
             "param_gather_bytes_per_step": int(gather_step),
             "exposed_comm_ms": round(exposed_ms, 3) if exposed_ms is not None else None,
+            "cpu_affinity_rank0": affinity,
+            "runtime": runtime_env(),
         }
         print(json.dumps(out), flush=True)
+    dump = os.environ.get("KOP_BENCH_DUMP_PARAMS")  # tests: the final parameters, layout order, no padding
+    if dump and info.is_main:
+        torch.save(torch.cat([p.detach().reshape(-1).float().cpu() for _, p in trainer.store.named_params()]), dump)
     shutdown(info)
     return 0
 

@@ -86,6 +86,70 @@ def init_distributed(device: str = "auto", timeout_s: int = 1800) -> DistInfo:
     return DistInfo(rank, dev_index if use_gpu else local, world, backend, dev)
 
 
+def parse_cpulist(text: str) -> list[int]:
+    """``0-3,8,10-11`` (sysfs ``local_cpulist``) -> [0, 1, 2, 3, 8, 10, 11]."""
+    out = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out += list(range(int(a), int(b or a) + 1))
+    return out
+
+
+def _gpu_pci_dir(index: int) -> str:
+    p = torch.cuda.get_device_properties(index)
+    return f"/sys/bus/pci/devices/{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+
+
+def _read(path: str) -> str:
+    with open(path) as f:
+        return f.read().strip()
+
+
+def bind_rank_cpus(info: DistInfo) -> dict | None:
+    """Pin this rank to the CPUs next to its GPU: the GPU's sysfs ``local_cpulist`` (its NUMA node), split
+    evenly among the local ranks whose GPUs share that list, intersected with the CPUs this process may use.
+    Multi-rank GPU jobs only (the one-GPU headline runs unpinned); ``KOP_CPU_AFFINITY=0`` turns it off.
+    Returns {"numa_node", "cpus"} (what was bound) or None."""
+    if info.device.type != "cuda" or info.world <= 1 or os.environ.get("KOP_CPU_AFFINITY", "1") == "0":
+        return None
+    try:
+        mine = _gpu_pci_dir(info.local_rank)
+        cpus = parse_cpulist(_read(mine + "/local_cpulist"))
+        numa = int(_read(mine + "/numa_node"))
+        nloc = int(os.environ.get("LOCAL_WORLD_SIZE", torch.cuda.device_count()))
+        peers = [i for i in range(min(nloc, torch.cuda.device_count()))
+                 if parse_cpulist(_read(_gpu_pci_dir(i) + "/local_cpulist")) == cpus]
+    except (OSError, ValueError, RuntimeError):
+        return None
+    allowed = os.sched_getaffinity(0)
+    if info.local_rank in peers and len(peers) > 1:
+        k, n = peers.index(info.local_rank), len(peers)
+        share = cpus[k * len(cpus) // n:(k + 1) * len(cpus) // n]
+    else:
+        share = cpus
+    want = [c for c in share if c in allowed] or [c for c in cpus if c in allowed]
+    if not want:
+        return None
+    os.sched_setaffinity(0, want)
+    return {"numa_node": numa, "cpus": f"{want[0]}-{want[-1]}" if want == list(range(want[0], want[-1] + 1))
+            else ",".join(map(str, want)), "ncpus": len(want)}
+
+
+def runtime_env() -> dict:
+    """Versions and communication environment of this process, for interpreting multi-GPU results."""
+    rccl = None
+    try:
+        v = torch.cuda.nccl.version()
+        rccl = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+    except Exception:  # noqa: BLE001 -- no RCCL in a CPU-only build
+        pass
+    keep = ("NCCL_", "RCCL_", "HSA_", "TORCH_NCCL_", "HIP_", "ROCR_", "GPU_MAX_HW_QUEUES", "OMP_NUM_THREADS")
+    return {"torch": torch.__version__, "hip": getattr(torch.version, "hip", None), "rccl": rccl,
+            "env": {k: os.environ[k] for k in sorted(os.environ) if k.startswith(keep)}}
+
+
 def barrier(info: DistInfo) -> None:
     if collectives_on(info):
         if info.backend == "nccl":

@@ -410,9 +410,11 @@ def test_elastic_restart_after_injected_rank_failure_resumes_exactly(tmp_path):
     ev = []
     for ln in bad.stdout.splitlines():  # the two ranks' lines may interleave around the crash
         try:
-            ev.append(json.loads(ln))
+            rec = json.loads(ln)
         except ValueError:
-            pass
+            continue
+        if isinstance(rec, dict):  # an interleaved fragment such as "12" parses as a JSON int
+            ev.append(rec)
     assert {"event": "resumed", "step": 2} in ev, bad.stdout
     assert '"injected_fault"' in bad.stdout
     assert [e["step"] for e in ev if "loss" in e][-1] == 6

@@ -259,6 +259,14 @@ class WorkerPool:
             s.execute(update(M.WorkerHeartbeat).where(M.WorkerHeartbeat.name == self.name)
                       .values(last_seen=M.now(), active=active, processed=processed, stopped=stopped))
 
+    def _safe_beat(self) -> None:
+        """A heartbeat inside the job loop: a store error (e.g. SQLite 'database is locked') is logged and never
+        stops the claimed job or kills the worker thread (the periodic loop beats again shortly)."""
+        try:
+            self._beat()
+        except Exception:  # noqa: BLE001
+            log.exception("worker heartbeat failed")
+
     def _heartbeat_loop(self):
         while not self._stop.wait(self.heartbeat_s):
             try:
@@ -275,14 +283,14 @@ class WorkerPool:
                 continue
             with self._lock:
                 self._active.add(job.id)
-            self._beat()
+            self._safe_beat()
             try:
                 run_job(job)
             finally:
                 with self._lock:
                     self._active.discard(job.id)
                     self._processed += 1
-                self._beat()
+                self._safe_beat()
 
     def stop(self, timeout: float = 5.0):
         self._stop.set()

@@ -764,7 +764,11 @@ __global__ void __launch_bounds__(NT) rms_bwd_t_kernel(const bf16_t* __restrict_
   reinterpret_cast<f32x4*>(dw_part + grp * H)[t] = f32x4{dwa[0], dwa[1], dwa[2], dwa[3]};
 }
 
-static bool t_shape_ok(int rows, int H) { return (H == 2048 || H == 4096) && rows % kTRG == 0 && rows > 0; }
+// the transposed kernels address through 32-bit buffer descriptors / offsets: refuse shapes whose bytes reach 2 GiB
+// (out-of-range buffer accesses would silently read 0 / drop stores); callers then take the plain norm kernels
+static bool t_shape_ok(int rows, int H) {
+  return (H == 2048 || H == 4096) && rows % kTRG == 0 && rows > 0 && (int64_t)rows * H * 2 < ((int64_t)1 << 31);
+}
 static int t_remap(int rows) { return (rows / kTRG) % 32 == 0 ? 1 : 0; }
 
 int rms_norm_t_parts(int rows, int H) { return t_shape_ok(rows, H) ? rows / kTRG : 0; }

@@ -325,9 +325,15 @@ def test_bigip_config_attaches_virtual_servers(control):
     assert deploy.create("demo", "install", run="inline")["state"] == "SUCCESS"
     clusters.set_config("demo", "bigip_url", "https://10.9.9.9")
     clusters.set_config("demo", "public_ip", "10.9.9.100")
+    evil = "p w;$(touch /tmp/pwned)'\""
+    clusters.set_config("demo", "bigip_password", evil)
+    start = len(control.farm.log)
     e = deploy.create("demo", "bigip-config", run="inline")
     assert e["state"] == "SUCCESS", e["result_summary"].get("dark")
     log = [c for _, c in control.farm.log]
+    # the credentials reach the secret through 0600 files, never through a shell command line
+    assert not [c for c in log[start:] if "touch /tmp/pwned" in c]
+    assert any("--from-file=password=/opt/kubeoperator/secrets/bigip/password" in c for c in log[start:])
     ann = [c for c in log if "annotate ingress" in c]
     for name in ("f2c-grafana", "registry-ui", "weave-scope", "kubeapps-plus", "dashboard-kubernetes-dashboard"):
         assert any(f" {name} " in c and "virtual-server.f5.com/ip=10.9.9.100" in c for c in ann), name

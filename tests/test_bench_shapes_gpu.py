@@ -92,6 +92,27 @@ def _check_bench_shape(B, S, Hq, Hkv, D):
         assert err < 3e-2, (name, err)
     # every query row was written: no workgroup of the remapped grid skipped (a dropped block leaves zeros)
     assert (o.float().abs().sum(1) > 0).all()
+    # no worse than plain bf16 PyTorch (SDPA) on the same inputs, whole tensor and smallest-norm (row, head) slices
+    from numerics import check_against_bf16
+
+    ob, gb = _sdpa_bf16(qkv.detach(), do, B, S, Hq, Hkv, D)
+    res = [check_against_bf16("o", o.reshape(-1, D), o_ref.reshape(-1, D), ob.reshape(-1, D))]
+    for name, sl in (("dq", slice(0, a)), ("dk", slice(a, c)), ("dv", slice(c, None))):
+        res.append(check_against_bf16(name, g[:, sl].reshape(-1, D), dqkv_ref[:, sl].reshape(-1, D),
+                                      gb[:, sl].reshape(-1, D)))
+    print("numerics vs plain bf16:", res)
+
+
+def _sdpa_bf16(qkv, do, B, S, Hq, Hkv, D):
+    x = qkv.detach().clone().requires_grad_(True)
+    a, c = Hq * D, (Hq + Hkv) * D
+    q = x[:, :a].reshape(B, S, Hq, D).transpose(1, 2)
+    k = x[:, a:c].reshape(B, S, Hkv, D).transpose(1, 2).repeat_interleave(Hq // Hkv, 1)
+    v = x[:, c:].reshape(B, S, Hkv, D).transpose(1, 2).repeat_interleave(Hq // Hkv, 1)
+    o = torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=True)
+    o = o.transpose(1, 2).reshape(B * S, a)
+    o.backward(do)
+    return o.detach().float(), x.grad.float()
 
 
 def test_rmsnorm_at_bench_shape():
@@ -114,6 +135,16 @@ def test_rmsnorm_at_bench_shape():
     assert rel_err(s, sf) < 1e-2
     assert rel_err(x.grad, xf.grad) < 3e-2
     assert rel_err(w.grad, wf.grad) < 3e-2  # column sum over 8192 rows (two-stage partials)
+    # plain bf16 PyTorch on the same inputs
+    from numerics import check_against_bf16
+
+    xb, rb, wb = (t.detach().clone().requires_grad_(True) for t in (x, r, w))
+    s_b = xb + rb
+    yb = s_b * torch.rsqrt(s_b.pow(2).mean(-1, keepdim=True) + 1e-5) * wb
+    ((yb * dy).sum() + (s_b * ds).sum()).backward()
+    check_against_bf16("y", y, yf, yb)
+    check_against_bf16("dx", x.grad, xf.grad, xb.grad)
+    check_against_bf16("dw", w.grad.reshape(1, -1), wf.grad.reshape(1, -1), wb.grad.reshape(1, -1))
 
 
 def test_cross_entropy_at_bench_shape():
@@ -134,3 +165,10 @@ def test_cross_entropy_at_bench_shape():
     assert abs(loss.item() - lf.item()) < 1e-2 * max(1.0, lf.item())
     assert rel_err(x.grad, xf.grad) < 3e-2
     assert rel_err(w.grad, wf.grad) < 3e-2
+    # plain bf16 PyTorch: bf16 logits, cross_entropy and its autograd on the same inputs
+    from numerics import check_against_bf16
+
+    xb, wb = (t.detach().clone().requires_grad_(True) for t in (x, w))
+    torch.nn.functional.cross_entropy(xb @ wb.t(), tgt, ignore_index=-100).backward()
+    check_against_bf16("dx", x.grad, xf.grad, xb.grad)
+    check_against_bf16("dw", w.grad, wf.grad, wb.grad)

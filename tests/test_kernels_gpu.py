@@ -206,6 +206,12 @@ def test_flash_attention_fwd(D, causal):
     o, lse, o_ref, lse_ref = _attn_case(2, 256, 8, 2, D, causal)
     assert rel_err(o, o_ref) < 2e-2
     assert (lse - lse_ref).abs().max().item() < 2e-2
+    from numerics import check_against_bf16
+
+    torch.manual_seed(7)  # the same qkv as _attn_case
+    qkv = torch.randn(2 * 256, (8 + 2 * 2) * D, device=DEV, dtype=torch.bfloat16)
+    ob, _ = _sdpa_bf16(qkv, torch.zeros(2 * 256, 8 * D, device=DEV), 2, 256, 8, 2, D, causal)
+    check_against_bf16("o", o.reshape(-1, D), o_ref.reshape(-1, D), ob.reshape(-1, D))
 
 
 @pytest.mark.parametrize("variant", [-1, 10, 8, 9, 0])
@@ -286,6 +292,26 @@ def test_flash_attention_bwd(D, Hq, Hkv, causal):
     g, gr = qkv.grad.float(), x.grad
     for name, sl in (("dq", slice(0, a)), ("dk", slice(a, c)), ("dv", slice(c, None))):
         assert rel_err(g[:, sl], gr[:, sl]) < 3e-2, name
+    # no worse than plain bf16 PyTorch on the same inputs (whole tensor and smallest-norm (row, head) slices)
+    from numerics import check_against_bf16
+
+    ob, gb = _sdpa_bf16(qkv.detach(), do, B, S, Hq, Hkv, D, causal)
+    check_against_bf16("o", o.reshape(-1, D), of.reshape(-1, D), ob.reshape(-1, D))
+    for name, sl in (("dq", slice(0, a)), ("dk", slice(a, c)), ("dv", slice(c, None))):
+        check_against_bf16(name, g[:, sl].reshape(-1, D), gr[:, sl].reshape(-1, D), gb[:, sl].reshape(-1, D))
+
+
+def _sdpa_bf16(qkv, do, B, S, Hq, Hkv, D, causal):
+    """Plain bf16 PyTorch attention (SDPA, GQA by repeat_interleave) forward + backward -> (o, dqkv)."""
+    x = qkv.detach().clone().requires_grad_(True)
+    a, c = Hq * D, (Hq + Hkv) * D
+    q = x[:, :a].reshape(B, S, Hq, D).transpose(1, 2)
+    k = x[:, a:c].reshape(B, S, Hkv, D).transpose(1, 2).repeat_interleave(Hq // Hkv, 1)
+    v = x[:, c:].reshape(B, S, Hkv, D).transpose(1, 2).repeat_interleave(Hq // Hkv, 1)
+    o = torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=causal)
+    o = o.transpose(1, 2).reshape(B * S, a)
+    o.backward(do.to(torch.bfloat16))
+    return o.detach(), x.grad
 
 
 def test_rope_attention_end_to_end_grad():

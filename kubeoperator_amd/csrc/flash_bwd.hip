@@ -807,12 +807,13 @@ static void launch_dq_ds(const bf16_t* ds, const bf16_t* k, bf16_t* dq, int B, i
                                                                                          ks, dqs, scale, causal);
 }
 
-// dk/dv = bf16(sum over the GQA group of the per-q-head partials)
+// dk/dv = bf16(sum of the NP per-group partials): partial p of KV head h at slot h * grp + p of [T, Hq, D]
+// (NP = grp when every q-head wrote its own; fewer when the dK/dV kernel swept several heads per workgroup)
 template <int D>
 __global__ void __launch_bounds__(256) fa_bwd_finalize_kernel(const float* __restrict__ dk_part,
                                                               const float* __restrict__ dv_part, bf16_t* __restrict__ dk,
                                                               bf16_t* __restrict__ dv, int64_t T, int Hq, int Hkv,
-                                                              int64_t dks, int64_t dvs) {
+                                                              int64_t dks, int64_t dvs, int np) {
   const int grp = Hq / Hkv;
   const int64_t nk = T * Hkv * (D / 8);
   for (int64_t it = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; it < nk; it += (int64_t)gridDim.x * blockDim.x) {
@@ -820,7 +821,7 @@ __global__ void __launch_bounds__(256) fa_bwd_finalize_kernel(const float* __res
     const int rem = (int)(it % (Hkv * (D / 8)));
     const int h = rem / (D / 8), c8 = rem % (D / 8);
     float fk[8] = {0, 0, 0, 0, 0, 0, 0, 0}, fv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int g = 0; g < grp; ++g) {
+    for (int g = 0; g < np; ++g) {
       const int64_t off = t * Hq * D + (int64_t)(h * grp + g) * D + c8 * 8;
       const f32x4* pk = reinterpret_cast<const f32x4*>(dk_part + off);
       const f32x4* pv = reinterpret_cast<const f32x4*>(dv_part + off);
@@ -960,9 +961,10 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
     const bool one_wave = S % 256 == 0 && ((D == 128 && (cfg == 64 || cfg == 66)) || (D == 64 && cfg == 640));
     const bool blk = one_wave && cfg != 66;
     bool done = false;
+    int np = direct ? 0 : Hq / Hkv;  // fp32 partials per GQA group left for the finalize pass
     if (one_wave) {
-      flash_attn_bwd_dkdv64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, D, qs, ks, vs, dos,
-                            dks, dvs, scale, cflag, true, blk, stream);
+      np = flash_attn_bwd_dkdv64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, D, qs, ks, vs,
+                                 dos, dks, dvs, scale, cflag, true, blk, stream);
       done = true;
     }
     if constexpr (D == 128) {
@@ -982,19 +984,19 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
                                dos, dks, dvs, scale, cflag, stream);
     if (blk) launch_dq_ds_hp<D, true>(hp, ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
     else launch_dq_ds_hp<D, false>(hp, ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-    if (!direct) fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs);
+    if (np > 0) fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs, np);
     return;
   }
+  int np = Hq / Hkv;
   if (D == 128 && dkdv_cfg() == 64 && S % 256 == 0) {
     // the one-wave dK/dV kernel without dS stores; dQ recomputes S and dP below. It writes bf16 dK / dV itself
     // when Hq == Hkv, so the finalize pass is then skipped.
-    flash_attn_bwd_dkdv64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, nullptr, B, S, Hq, Hkv, D, qs, ks,
-                          vs, dos, dks, dvs, scale, causal ? 1 : 0, false, false, stream);
+    np = flash_attn_bwd_dkdv64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, nullptr, B, S, Hq, Hkv, D, qs, ks,
+                               vs, dos, dks, dvs, scale, causal ? 1 : 0, false, false, stream);
   } else {
     fa_bwd_dkdv_kernel<D, NW, false><<<B * Hq * (S / (32 * NW)), NW * 64, lds_kv, stream>>>(
         q, k, v, dout, nlse, ndelta, dk_part, dv_part, nullptr, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal);
   }
-  const bool direct64 = D == 128 && dkdv_cfg() == 64 && S % 256 == 0 && Hq == Hkv;
   if (S % 256 == 0 && variant >= 8) {
     const bool stg = variant != 8;
     const size_t lds8 = (stg ? 4 : 3) * 2 * 64 * (D * 2);
@@ -1016,7 +1018,7 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
     fa_bwd_dq_kernel<D, NW><<<B * Hq * (S / (32 * NW)), NW * 64, lds_q, stream>>>(
         q, k, v, dout, lse, delta, dq, B, S, Hq, Hkv, qs, ks, vs, dos, dqs, scale, causal);
   }
-  if (!direct64) fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs);
+  if (np > 0) fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs, np);
 }
 
 int flash_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,

@@ -94,7 +94,11 @@ __device__ __forceinline__ void vm_wait_le(int n) {
 // REV: sweep the query stages from the last one down to the workgroup's diagonal. Every workgroup of a head then
 // reads the same Q / dO stage at the same time (forward order starts workgroup kb 8*kb stages later, so a stage is
 // re-read ~16 us apart -- long enough for the dS write stream to evict it from the XCD's 4 MB L2).
-template <int D, bool DIRECT, int NS, bool QM, int DIAG = 0, bool BLK = false, bool REV = false>
+// HPW: query heads of one GQA group swept by the workgroup one after the other, accumulating into the same dK^T /
+// dV^T registers (their keys and values are shared). HPW == the group size (DIRECT) writes bf16 dK / dV outright;
+// otherwise the workgroup writes one fp32 partial per HPW heads (slot kvh * grp + part of [T, Hq, D]) and
+// fa_bwd_finalize_kernel sums grp / HPW partials.
+template <int D, bool DIRECT, int NS, bool QM, int DIAG = 0, bool BLK = false, bool REV = false, int HPW = 1>
 __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ nlse, const float* __restrict__ ndelta,
@@ -113,41 +117,40 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hh = lane >> 5;
   const int tq = (lane & 15) >> 2, tp = lane & 3, tg1 = (lane >> 4) & 1;
-  const int nkb = S / BN;
-  const AttnWork aw = attn_work(blockIdx.x, B, Hq, Hq / Hkv, nkb);
+  const int nkb = S / BN, grp = Hq / Hkv;
+  const AttnWork aw = attn_work(blockIdx.x, B, Hq / HPW, grp / HPW, nkb);
   const int kb = aw.rank;  // heaviest key blocks (earliest keys under a causal mask) first
-  const int b = aw.b, hq = aw.unit;
-  const int kvh = hq / (Hq / Hkv);
+  const int b = aw.b, hq0 = aw.unit * HPW;
+  const int kvh = hq0 / grp;
   const int k0 = kb * BN, k0w = k0 + KW * wid;
   const float c2 = scale * 1.4426950408889634f;
-
-  const float* lse_h = nlse + ((int64_t)(b * Hq + hq)) * S;
-  const float* del_h = ndelta + ((int64_t)(b * Hq + hq)) * S;
-  const bf16_t* qbase = q + (int64_t)(b * S) * qs + hq * D;
-  const bf16_t* dobase = dout + (int64_t)(b * S) * dos + hq * D;
   const int qt0 = causal ? k0 / BQ : 0;
   const int nqt = S / BQ;
+  // the sweep: HPW heads x nst query stages, sequence index sq -> (head hq0 + sq / nst, stage of the order below)
+  const int nst = nqt - qt0, tot = HPW * nst;
+  auto s_qt = [&](int sq) {
+    const int i = sq % nst;
+    return REV ? nqt - 1 - i : qt0 + i;
+  };
 
-  auto issue = [&](int qt) {
-    char* base = smem + KB + ((qt - qt0) % NS) * STAGE;
-    const int q0 = qt * BQ;
-    dma_tile_a<ROWB, NW, BQ>(base, qbase + (int64_t)q0 * qs, qs, wid, lane);
-    dma_tile_a<ROWB, NW, BQ>(base + QT, dobase + (int64_t)q0 * dos, dos, wid, lane);
+  auto issue = [&](int sq) {
+    char* base = smem + KB + (sq % NS) * STAGE;
+    const int hq = hq0 + sq / nst;
+    const int q0 = s_qt(sq) * BQ;
+    dma_tile_a<ROWB, NW, BQ>(base, q + (int64_t)(b * S + q0) * qs + hq * D, qs, wid, lane);
+    dma_tile_a<ROWB, NW, BQ>(base + QT, dout + (int64_t)(b * S + q0) * dos + hq * D, dos, wid, lane);
     if (wid == 0) {
       const int l = lane & 15;
-      const float* src = (l < 8 ? lse_h + q0 + 4 * l : del_h + q0 + 4 * (l - 8));
+      const int64_t rowh = ((int64_t)(b * Hq + hq)) * S + q0;
+      const float* src = (l < 8 ? nlse + rowh + 4 * l : ndelta + rowh + 4 * (l - 8));
       glds16(src, base + 2 * QT);
     }
   };
   dma_tile_a<ROWB, NW, BN>(Kl, k + (int64_t)(b * S + k0) * ks + kvh * D, ks, wid, lane);
-  // stage order: qt0, qt0 + 1, ... (forward) or nqt - 1, nqt - 2, ... (REV); nxt(qt, i) is i stages later
-  auto nxt = [&](int x, int i) { return REV ? x - i : x + i; };
-  auto valid = [&](int x) { return REV ? x >= qt0 : x < nqt; };
-  const int first = REV ? nqt - 1 : qt0;
-  issue(first);
+  issue(0);
 #pragma unroll
   for (int i = 1; i < NS - 1; ++i)
-    if (valid(nxt(first, i))) issue(nxt(first, i));
+    if (i < tot) issue(i);
 
   const int rb_lane0 = RB * (r >> 3) + 64 * (r & 7) + 16 * (hh ^ ((r >> 2) & 3));
   const int rb_lane1 = RB * (r >> 3) + 64 * (r & 7) + 16 * ((2 + hh) ^ ((r >> 2) & 3));
@@ -172,8 +175,8 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
 
   const int pcount = MYP + (wid == 0 ? 1 : 0);  // DMA ops this wave issues per stage
   int st1 = 0, st2 = 0;                           // dS stores issued in the previous / second-previous stage
-  // dS^T rows of the wave's keys: row pointer in SGPRs, lane offset (key r, queries 16s + 8hh) in one VGPR
-  const uint64_t dsrow = (uint64_t)(uintptr_t)(dst + ((int64_t)(b * Hq + hq) * S + k0w) * S);
+  // dS^T rows of the wave's keys: row pointer in SGPRs (per head), lane offset (key r, queries 16s + 8hh) in one VGPR
+  auto dsrow_of = [&](int hq) { return (uint64_t)(uintptr_t)(dst + ((int64_t)(b * Hq + hq) * S + k0w) * S); };
   const uint32_t dsoff = 2u * (uint32_t)(r * S + 8 * hh);
   // QM staging image of the wave's stage tile: [64 keys][32 queries] bf16, 64-B rows, 16-B chunks XOR-swizzled
   // by (key >> 1) & 3. Writes: lane (key r of block c, queries 16s + 8hh ..) -> chunk 2s + hh. Transposed reads:
@@ -185,29 +188,34 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
   const int sg = lane >> 4, si = lane & 15, sq = si >> 2, sp = si & 3;
   const int skey = 4 * (sg >> 1) + sq;
   const uint32_t str = lds_addr(stg) + 64 * skey + 16 * ((2 * (sg & 1) + (sp >> 1)) ^ ((skey >> 1) & 3)) + 8 * (sp & 1);
-  const uint64_t dsq = BLK ? (uint64_t)(uintptr_t)(dst + ((int64_t)(b * Hq + hq) * (S / 32) * (S / 64) + k0w / 64) * 2048)
-                          : (uint64_t)(uintptr_t)(dst + ((int64_t)(b * Hq + hq) * S) * S + k0w);
+  auto dsq_of = [&](int hq) {
+    return BLK ? (uint64_t)(uintptr_t)(dst + ((int64_t)(b * Hq + hq) * (S / 32) * (S / 64) + k0w / 64) * 2048)
+               : (uint64_t)(uintptr_t)(dst + ((int64_t)(b * Hq + hq) * S) * S + k0w);
+  };
   const uint32_t sqoff = BLK ? 2u * (uint32_t)((16 * (sg & 1) + si) * 64 + 8 * (sg >> 1))
                              : 2u * (uint32_t)((16 * (sg & 1) + si) * S + 8 * (sg >> 1));
-  (void)stw0; (void)stw1; (void)str; (void)dsq; (void)sqoff;
+  (void)stw0; (void)stw1; (void)str; (void)sqoff;
 
-  auto body = [&](int qt, auto mask_c) {
+  auto body = [&](int sq, auto mask_c) {
     constexpr bool MASK = decltype(mask_c)::value;
-    // DMA(qt) is older than: stores(qt-2), DMA(qt+NS-2), stores(qt-1) (and the other DMAs still in flight)
+    const int qt = s_qt(sq), hq = hq0 + sq / nst;
+    const uint64_t dsrow = dsrow_of(hq), dsq = dsq_of(hq);
+    (void)dsrow; (void)dsq;
+    // DMA(sq) is older than: stores(sq-2), DMA(sq+NS-2), stores(sq-1) (and the other DMAs still in flight)
     int younger = st1 + st2;
 #pragma unroll
-    for (int i = 1; i < NS - 1; ++i) younger += valid(nxt(qt, i)) ? pcount : 0;
+    for (int i = 1; i < NS - 1; ++i) younger += (sq + i < tot) ? pcount : 0;
     if constexpr (!(DIAG & 36)) vm_wait_le(younger);
     st2 = st1;
     st1 = 0;
     if constexpr (!(DIAG & 8)) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if constexpr (!(DIAG & 4)) {
-      if (valid(nxt(qt, NS - 1))) issue(nxt(qt, NS - 1));
+      if (sq + NS - 1 < tot) issue(sq + NS - 1);
     }
     const int qs0 = qt * BQ;
     if (causal && qs0 + BQ - 1 < k0w) return;  // every query of the stage precedes every key of the wave
-    const char* Ql = smem + KB + ((qt - qt0) % NS) * STAGE;
+    const char* Ql = smem + KB + (sq % NS) * STAGE;
     const char* Ol = Ql + QT;
     // Every LDS read below is an inline-asm read retired by a counted lgkmcnt, and every step ends in
     // sched_barrier(0): left to itself hipcc sank the MFMAs below later reads, which serialised them (one wave
@@ -427,15 +435,20 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     }
     asm volatile("" ::: "memory");
   };
-  // the causal mask is needed only in the first BN / BQ stages of the forward order
+  // the causal mask is needed only in the BN / BQ stages nearest the diagonal (qt < qd)
   const int qd = causal ? (qt0 + BN / BQ < nqt ? qt0 + BN / BQ : nqt) : qt0;
-  if constexpr (REV) {
-    for (int qt = nqt - 1; qt >= qd; --qt) body(qt, std::false_type{});
-    for (int qt = qd - 1; qt >= qt0; --qt) body(qt, std::true_type{});
-  } else {
-    int qt = qt0;
-    for (; qt < qd; ++qt) body(qt, std::true_type{});
-    for (; qt < nqt; ++qt) body(qt, std::false_type{});
+  // per head: two loops (unmasked / masked stages) -- one loop with a branch between the two body instantiations
+  // made hipcc spill ~500 VGPRs
+  for (int hi = 0; hi < HPW; ++hi) {
+    const int s0 = hi * nst;
+    if constexpr (REV) {
+      for (int qt = nqt - 1; qt >= qd; --qt) body(s0 + (nqt - 1 - qt), std::false_type{});
+      for (int qt = qd - 1; qt >= qt0; --qt) body(s0 + (nqt - 1 - qt), std::true_type{});
+    } else {
+      int qt = qt0;
+      for (; qt < qd; ++qt) body(s0 + (qt - qt0), std::true_type{});
+      for (; qt < nqt; ++qt) body(s0 + (qt - qt0), std::false_type{});
+    }
   }
   // the accumulators leave the AGPRs through compiler v_accvgpr_read: 18 wait states after the last 16-pass MFMA
   // that wrote them (hipcc pads nothing after an asm MFMA)
@@ -446,8 +459,8 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
 
   auto out = [&](const f32x16* dka, const f32x16* dva, int key) {
     if constexpr (DIRECT) {
-      bf16_t* dkb = reinterpret_cast<bf16_t*>(dk_part) + (int64_t)(b * S + key) * dks + hq * D;
-      bf16_t* dvb = reinterpret_cast<bf16_t*>(dv_part) + (int64_t)(b * S + key) * dvs + hq * D;
+      bf16_t* dkb = reinterpret_cast<bf16_t*>(dk_part) + (int64_t)(b * S + key) * dks + kvh * D;
+      bf16_t* dvb = reinterpret_cast<bf16_t*>(dv_part) + (int64_t)(b * S + key) * dvs + kvh * D;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
 #pragma unroll
@@ -461,8 +474,9 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
         }
       }
     } else {
-      float* dkp = dk_part + (int64_t)(b * S + key) * Hq * D + hq * D;
-      float* dvp = dv_part + (int64_t)(b * S + key) * Hq * D + hq * D;
+      const int slot = kvh * grp + (hq0 % grp) / HPW;  // this workgroup's partial of the group
+      float* dkp = dk_part + (int64_t)(b * S + key) * Hq * D + slot * D;
+      float* dvp = dv_part + (int64_t)(b * S + key) * Hq * D + slot * D;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
 #pragma unroll
@@ -480,36 +494,60 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
   out(dk1, dv1, k0w + 32 + r);
 }
 
+// heads per workgroup: the largest power of two dividing the GQA group that still leaves >= 2 workgroups per CU
+// (the causal key blocks differ 32x in work; fewer, longer workgroups would end on a few heavy ones).
+// KOP_DKDV_HPW overrides (1 / 2 / 4 / 8).
+static int pick_hpw(int B, int S, int Hq, int Hkv) {
+  static const int env = [] {
+    const char* e = getenv("KOP_DKDV_HPW");
+    return e ? atoi(e) : 0;
+  }();
+  const int grp = Hq / Hkv;
+  if (env > 0) return (grp % env == 0 && env <= 8) ? env : 1;
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  int h = 1;
+  while (h * 2 <= 8 && grp % (h * 2) == 0 && (int64_t)B * (Hq / (h * 2)) * (S / 256) >= 2 * (int64_t)cus) h *= 2;
+  return h;
+}
+
 template <int D>
-static void dkdv64_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout, const float* nlse,
-                          const float* ndelta, float* dk_part, float* dv_part, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B,
-                          int S, int Hq, int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t dos, int64_t dks,
-                          int64_t dvs, float scale, int causal, bool qm, bool blk_layout, hipStream_t stream) {
+static int dkdv64_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout, const float* nlse,
+                         const float* ndelta, float* dk_part, float* dv_part, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B,
+                         int S, int Hq, int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t dos, int64_t dks,
+                         int64_t dvs, float scale, int causal, bool qm, bool blk_layout, hipStream_t stream) {
   constexpr int NS = 3;
   const size_t lds = 256 * (D * 2) + NS * (2 * 32 * (D * 2) + 1024) + 4 * 4096;
-  const dim3 grid(B * Hq * (S / 256));
+  const int grp = Hq / Hkv;
   static const int diag = [] {
     const char* e = getenv("KOP_DKDV64_DIAG");
     return e ? atoi(e) : 0;
   }();
-  // one instantiation per (DIRECT, QM, DIAG) actually launched; the dynamic-LDS attribute is set on first use
-#define KOP_LAUNCH(DIR, QMV, DG, BL) KOP_LAUNCH_R(DIR, QMV, DG, BL, true)
-#define KOP_LAUNCH_FWD(DIR, QMV, DG, BL) KOP_LAUNCH_R(DIR, QMV, DG, BL, false)
-#define KOP_LAUNCH_R(DIR, QMV, DG, BL, RV)                                                                              \
+  // one instantiation per (DIRECT, QM, DIAG, BLK, REV, HPW) actually launched; the dynamic-LDS attribute is set on
+  // first use. Returns the number of partials per GQA group the finalize pass must sum (0: dK / dV written).
+#define KOP_LAUNCH(DIR, QMV, DG, BL) KOP_LAUNCH_R(DIR, QMV, DG, BL, true, 1)
+#define KOP_LAUNCH_FWD(DIR, QMV, DG, BL) KOP_LAUNCH_R(DIR, QMV, DG, BL, false, 1)
+#define KOP_LAUNCH_R(DIR, QMV, DG, BL, RV, HP)                                                                         \
   do {                                                                                                             \
     static bool attr = false;                                                                                      \
     if (!attr) {                                                                                                   \
-      (void)hipFuncSetAttribute((const void*)fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG, BL, RV>,                              \
+      (void)hipFuncSetAttribute((const void*)fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG, BL, RV, HP>,                 \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                             \
       attr = true;                                                                                                 \
     }                                                                                                              \
+    const dim3 grid(B * (Hq / HP) * (S / 256));                                                                    \
     if (DIR)                                                                                                       \
-      fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG, BL, RV><<<grid, 256, lds, stream>>>(                                \
+      fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG, BL, RV, HP><<<grid, 256, lds, stream>>>(                             \
           q, k, v, dout, nlse, ndelta, reinterpret_cast<float*>(dk), reinterpret_cast<float*>(dv), ds, B, S, Hq, Hkv, \
           qs, ks, vs, dos, scale, causal, dks, dvs);                                                               \
     else                                                                                                           \
-      fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG, BL, RV><<<grid, 256, lds, stream>>>(                                \
+      fa_bwd_dkdv64_kernel<D, DIR, NS, QMV, DG, BL, RV, HP><<<grid, 256, lds, stream>>>(                             \
           q, k, v, dout, nlse, ndelta, dk_part, dv_part, ds, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal, 0, 0);  \
+    return (DIR) ? 0 : grp / (HP);                                                                                 \
   } while (0)
   static const bool rev = [] {
     const char* e = getenv("KOP_DKDV_REV");  // reversed stage sweep (default on); 0: forward order
@@ -517,44 +555,52 @@ static void dkdv64_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, con
   }();
   if (diag != 0 && Hq != Hkv && qm && ds != nullptr) {
     switch (diag) {
-      case 1: KOP_LAUNCH(false, true, 1, false); return;
-      case 2: KOP_LAUNCH(false, true, 2, false); return;
-      case 4: KOP_LAUNCH(false, true, 4, false); return;
-      case 8: KOP_LAUNCH(false, true, 8, false); return;
-      case 16: KOP_LAUNCH(false, true, 16, false); return;
-      case 32: KOP_LAUNCH(false, true, 32, false); return;
-      case 48: KOP_LAUNCH(false, true, 48, false); return;
+      case 1: KOP_LAUNCH(false, true, 1, false);
+      case 2: KOP_LAUNCH(false, true, 2, false);
+      case 4: KOP_LAUNCH(false, true, 4, false);
+      case 8: KOP_LAUNCH(false, true, 8, false);
+      case 16: KOP_LAUNCH(false, true, 16, false);
+      case 32: KOP_LAUNCH(false, true, 32, false);
+      case 48: KOP_LAUNCH(false, true, 48, false);
       default: break;
     }
   }
   if (ds == nullptr) {  // no dS at all (dQ recomputes it): the store-free build
     if (Hq == Hkv) KOP_LAUNCH(true, true, 1, false);
     else KOP_LAUNCH(false, true, 1, false);
-  } else if (!rev && Hq != Hkv) {  // forward stage order (A/B)
+  }
+  if (!rev && Hq != Hkv) {  // forward stage order (A/B)
     if (blk_layout) KOP_LAUNCH_FWD(false, true, 0, true);
     else KOP_LAUNCH_FWD(false, true, 0, false);
-  } else if (Hq == Hkv) {
+  }
+  if (Hq == Hkv) {
     if (blk_layout) KOP_LAUNCH(true, true, 0, true);
     else KOP_LAUNCH(true, true, 0, false);
-  } else {
-    if (blk_layout) KOP_LAUNCH(false, true, 0, true);
-    else KOP_LAUNCH(false, true, 0, false);
   }
+  const int hpw = pick_hpw(B, S, Hq, Hkv);
+  if (blk_layout) {
+    switch (hpw) {
+      case 2: if (grp == 2) KOP_LAUNCH_R(true, true, 0, true, true, 2); else KOP_LAUNCH_R(false, true, 0, true, true, 2);
+      case 4: if (grp == 4) KOP_LAUNCH_R(true, true, 0, true, true, 4); else KOP_LAUNCH_R(false, true, 0, true, true, 4);
+      case 8: if (grp == 8) KOP_LAUNCH_R(true, true, 0, true, true, 8); else KOP_LAUNCH_R(false, true, 0, true, true, 8);
+      default: KOP_LAUNCH(false, true, 0, true);
+    }
+  }
+  KOP_LAUNCH(false, true, 0, false);
 #undef KOP_LAUNCH
 #undef KOP_LAUNCH_FWD
 #undef KOP_LAUNCH_R
 }
 
-void flash_attn_bwd_dkdv64(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout, const float* nlse,
-                           const float* ndelta, float* dk_part, float* dv_part, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B,
-                           int S, int Hq, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t dos, int64_t dks,
-                           int64_t dvs, float scale, int causal, bool qm, bool blk_layout, hipStream_t stream) {
+int flash_attn_bwd_dkdv64(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout, const float* nlse,
+                          const float* ndelta, float* dk_part, float* dv_part, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B,
+                          int S, int Hq, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t dos, int64_t dks,
+                          int64_t dvs, float scale, int causal, bool qm, bool blk_layout, hipStream_t stream) {
   if (D == 128)
-    dkdv64_launch<128>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs, dos, dks,
-                       dvs, scale, causal, qm, blk_layout, stream);
-  else
-    dkdv64_launch<64>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs, dos, dks,
-                      dvs, scale, causal, qm, blk_layout, stream);
+    return dkdv64_launch<128>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs, dos,
+                              dks, dvs, scale, causal, qm, blk_layout, stream);
+  return dkdv64_launch<64>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs, dos, dks,
+                           dvs, scale, causal, qm, blk_layout, stream);
 }
 
 }  // namespace kop

@@ -81,8 +81,9 @@ int flash_attn_set_dkdv_cfg(int c);
 int flash_attn_set_fwd_variant(int v);
 // one-wave-per-SIMD dK/dV kernel (flash_bwd_w1.hip), D = 128 or 64, S % 256 == 0. ds: the query-major dS that
 // fa_bwd_dq_ds_kernel reads (blk_layout: its wave-block form), or nullptr for the store-free build (dQ recomputed);
-// qm is kept for the call sites and must be true when ds is set
-void flash_attn_bwd_dkdv64(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout, const float* nlse,
+// qm is kept for the call sites and must be true when ds is set. Returns the number of fp32 dK / dV partials per
+// GQA group left in dk_part / dv_part for fa_bwd_finalize_kernel (0: bf16 dK / dV written to dk / dv directly).
+int flash_attn_bwd_dkdv64(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout, const float* nlse,
                            const float* ndelta, float* dk_part, float* dv_part, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B,
                            int S, int Hq, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t dos, int64_t dks,
                            int64_t dvs, float scale, int causal, bool qm, bool blk_layout, hipStream_t stream);

@@ -753,7 +753,8 @@ class Runner:
                 break
             ok = evaluate(t["until"], vv)
             if ok:
-                res["failed"] = False if "failed_when" not in t else res["failed"]
+                # as Ansible: the until condition ends the retries; the result still fails if the module failed
+                # (a non-zero rc) and no failed_when overrides that -- a met condition never hides a failing command
                 break
             if attempt >= max(1, retries):
                 res["failed"] = True

@@ -137,6 +137,31 @@ def test_runner_failure_rescue_ignore_until(tmp_path):
     assert cmds.count("flaky") == 3 and "echo rescued" in cmds and "echo always" in cmds and "echo after" in cmds
 
 
+def test_until_met_does_not_hide_a_failing_command(tmp_path):
+    """Ansible semantics: ``until`` ends the retries, but a command that exits non-zero still fails the task
+    unless ``failed_when`` says otherwise (the count is printed, then the pipeline fails)."""
+    t = FakeTransport()
+    t.add_rule(r"^count$", rc=1, stdout="8")
+    t.add_rule(r"^count2$", rc=1, stdout="8")
+    res, t, _ = _play(tmp_path, """
+    - hosts: kube-master
+      gather_facts: false
+      tasks:
+        - shell: count2
+          register: c2
+          until: c2.stdout | int >= 8
+          failed_when: c2.stdout | int < 8
+        - shell: count
+          register: c
+          until: c.stdout | int >= 8
+          retries: 2
+          delay: 0
+        - shell: "echo after"
+    """, transport=t)
+    assert not res["summary"]["success"]
+    assert "echo after" not in t.commands("m1") and t.commands("m1").count("count") == 1
+
+
 def test_runner_failure_stops_host_and_unreachable(tmp_path):
     t = FakeTransport()
     t.add_rule(r"^boom$", rc=2, hosts=("w1",))

@@ -54,7 +54,12 @@ def test_gather_info_finds_the_mi355x(local_control):
         assert g["arch"] == "gfx950", g
         assert g["device_id"] == "1002:" + _sysfs(g["pci"], "device")[2:], g
         assert _sysfs(g["pci"], "vendor") == "0x1002"
-        assert "kfd_node" in g and g["cu_count"] == 256, g
+    # the kfd topology exposes the properties of the GPUs this job may use (the others read empty on a shared
+    # host): those are merged by BDF and carry the CU count and the amd-smi index
+    usable = [g for g in h["gpus"] if "kfd_node" in g]
+    assert usable, h["gpus"]
+    for g in usable:
+        assert g["cu_count"] == 256 and g["arch"] == "gfx950" and "index" in g, g
 
 
 def test_gpu_check_tasks_pass_on_the_box(local_control):

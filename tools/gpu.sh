@@ -24,6 +24,7 @@
 #   tune-decode  TunableOp tuning of the decode GEMMs, then the decode benchmark
 #   serve        serving tests, decode benchmark, continuous-batching benchmark
 #   fp8          FP8 GPU tests and the opt-in --fp8 Llama-3-8B bench
+#   roofline     every library GEMM of the Llama-3-8B step, in-step vs isolated, with power / clock samples
 source "$(dirname "$0")/gpu_lib.sh"
 mkdir -p gpurun_out/prof gpurun_out/pmc
 
@@ -190,7 +191,11 @@ s_fp8() {
   step fp8_bench 400 $L8B --fp8 1
 }
 
-[ $# -gt 0 ] || { sed -n '2,22p' tools/gpu.sh; exit 2; }
+s_roofline() {
+  step gemm_roofline 900 python tools/gemm_roofline.py --out gpurun_out/gemm_roofline.jsonl
+}
+
+[ $# -gt 0 ] || { sed -n '2,23p' tools/gpu.sh; exit 2; }
 for s in "$@"; do
   fn="s_${s//-/_}"
   declare -F "$fn" > /dev/null || { echo "unknown session: $s"; exit 2; }

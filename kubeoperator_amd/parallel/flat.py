@@ -26,7 +26,6 @@ streams underneath the compute-bound forward GEMMs of step k+1 instead of runnin
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass, field
 
 import torch
@@ -96,42 +95,6 @@ class GradHooks:
         k = id(p)
         self.writes[k] = self.writes.get(k, 0) + 1
         self.store._param_written(p)
-
-
-def _hip_runtime():
-    """The HIP runtime library this process's torch uses (ctypes handle of the already-loaded libamdhip64)."""
-    import ctypes
-
-    with open("/proc/self/maps") as f:
-        paths = {ln.split()[-1] for ln in f if "libamdhip64.so" in ln}
-    return ctypes.CDLL(sorted(paths)[0] if paths else "libamdhip64.so")
-
-
-def _cu_masked_stream(device, fraction: str):
-    """A side stream whose kernels may only use ``fraction`` of the CUs (``hipExtStreamCreateWithCUMask``), the rest
-    staying free for the compute stream's memory-bound kernels; the mask drops whole bytes of each 32-bit word, so
-    every XCD keeps the same share (bit i of the mask is CU i, interleaved or contiguous across the 8 XCDs).
-    Empty / invalid ``fraction``: an ordinary stream."""
-    try:
-        f = float(fraction)
-    except ValueError:
-        return torch.cuda.Stream(device=device)
-    if not (0.0 < f < 1.0) or device.type != "cuda":
-        return torch.cuda.Stream(device=device)
-    import ctypes
-
-    n_cu = torch.cuda.get_device_properties(device).multi_processor_count
-    keep_bytes = max(1, min(3, round(4 * f)))  # bytes of 8 CUs kept per 32-CU word
-    word = (1 << (8 * keep_bytes)) - 1
-    nwords = (n_cu + 31) // 32
-    masks = (ctypes.c_uint32 * nwords)(*([word] * nwords))
-    lib = _hip_runtime()
-    handle = ctypes.c_void_p()
-    with torch.cuda.device(device):
-        rc = lib.hipExtStreamCreateWithCUMask(ctypes.byref(handle), ctypes.c_uint32(nwords), masks)
-    if rc != 0:
-        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
-    return torch.cuda.ExternalStream(handle.value, device=device)
 
 
 class FlatParamStore:
@@ -282,7 +245,7 @@ class FlatParamStore:
     # weight-gradient stream ---------------------------------------------------------------------
     def side_stream(self):
         if self._side is None:
-            self._side = _cu_masked_stream(self.device, os.environ.get("KOP_SIDE_CU_FRACTION", ""))
+            self._side = torch.cuda.Stream(device=self.device)
         return self._side
 
     def hold_side(self, tensors) -> None:

@@ -85,7 +85,9 @@ def port_conflicts(pkgs: list[dict]) -> dict[str, str]:
     port (reference package_manage.py:31-45 maps each package's container to its own ports)."""
     claimed: dict[int, str] = {}
     bad: dict[str, str] = {}
-    for p in sorted(pkgs, key=lambda x: x["name"]):
+    # packages with content first (by name), then the built-in metas: a built-in (nothing to serve) never takes a
+    # port away from a package dropped into PACKAGE_DIR
+    for p in sorted(pkgs, key=lambda x: (x.get("path") == "builtin", x["name"])):
         ports = _ports(p.get("meta") or {})
         if ports["repo_port"] == ports["registry_port"]:
             bad[p["name"]] = f"repo_port and registry_port are both {ports['repo_port']}"

@@ -74,17 +74,37 @@ class OCILayout:
         self.media: dict[str, str] = {}  # manifest digest -> media type
         self._hash_cache: dict[str, tuple[int, float, str]] = {}
         self._hash_lock = threading.Lock()
+        self._load_lock = threading.Lock()
+        self._index_mtime = None
         self.load()
+
+    def refresh(self) -> None:
+        """Re-read ``index.json`` when it changed (images added to the package while it is served)."""
+        try:
+            m = os.stat(os.path.join(self.root, "index.json")).st_mtime_ns
+        except OSError:
+            return
+        if m != self._index_mtime:
+            with self._load_lock:
+                if m != self._index_mtime:
+                    self.load()
 
     def blob_path(self, digest: str) -> str:
         algo, _, hexd = digest.partition(":")
         return os.path.join(self.root, "blobs", algo, hexd)
 
     def load(self) -> None:
-        self.tags.clear()
-        self.reachable.clear()
-        with open(os.path.join(self.root, "index.json")) as f:
+        path = os.path.join(self.root, "index.json")
+        self._index_mtime = os.stat(path).st_mtime_ns
+        with open(path) as f:
             index = json.load(f)
+        # build the new tables aside, then swap them in: a request in flight sees the old or the new index, whole
+        tags: dict[str, dict[str, dict]] = {}
+        reach: dict[str, set[str]] = {}
+        self._index(index, tags, reach)
+        self.tags, self.reachable = tags, reach
+
+    def _index(self, index: dict, tags: dict, reach: dict) -> None:
         for d in index.get("manifests", []):
             ann = d.get("annotations") or {}
             parsed = None
@@ -96,12 +116,12 @@ class OCILayout:
             if not parsed or not _DIGEST_RE.match(d.get("digest", "")):
                 continue
             name, tag = parsed
-            self.tags.setdefault(name, {})[tag] = d
+            tags.setdefault(name, {})[tag] = d
             self.media[d["digest"]] = d.get("mediaType", OCI_MANIFEST)
-            self._walk(name, d["digest"])
+            self._walk(name, d["digest"], reach)
 
-    def _walk(self, name: str, digest: str) -> None:
-        seen = self.reachable.setdefault(name, set())
+    def _walk(self, name: str, digest: str, reach: dict) -> None:
+        seen = reach.setdefault(name, set())
         if digest in seen:
             return
         seen.add(digest)
@@ -114,7 +134,7 @@ class OCILayout:
             for child in body.get("manifests", []):
                 if _DIGEST_RE.match(child.get("digest", "")):
                     self.media[child["digest"]] = child.get("mediaType", OCI_MANIFEST)
-                    self._walk(name, child["digest"])
+                    self._walk(name, child["digest"], reach)
 
     def verified_digest(self, digest: str) -> bool:
         """True if the blob file exists and hashes to ``digest`` (hash cached by size + mtime)."""
@@ -188,6 +208,7 @@ class _RegistryHandler(http.server.BaseHTTPRequestHandler):
 
     # ---------------------------------------------------------------------------------------- routing
     def _route(self, head: bool) -> None:
+        self.layout.refresh()
         path = urllib.parse.urlsplit(self.path).path
         if path in ("/v2", "/v2/"):
             return self._send(200, b"{}", head=head)

@@ -195,6 +195,29 @@ def test_package_list_reports_endpoints_and_new_packages_are_served(served):
     assert _get(f"http://127.0.0.1:{gp2}/v2/")[0] == 200
 
 
+def test_registry_picks_up_images_added_while_serving(served):
+    pkg, _, gp, _, _ = served
+    reg = os.path.join(pkg["root"], "registry")
+    extra, _, _ = _manifest(reg, OCI_MANIFEST, "amd64")
+    with open(os.path.join(reg, "index.json")) as f:
+        idx = json.load(f)
+    idx["manifests"].append({**extra, "annotations": {"org.opencontainers.image.ref.name": "rocm/rocm-terminal:7.1"}})
+    with open(os.path.join(reg, "index.json"), "w") as f:
+        json.dump(idx, f)
+    st, h, _ = _get(f"http://127.0.0.1:{gp}/v2/rocm/rocm-terminal/manifests/7.1", "HEAD", {"Accept": OCI_MANIFEST})
+    assert st == 200 and h["Docker-Content-Digest"] == extra["digest"]
+
+
+def test_a_builtin_meta_never_takes_a_port_from_a_served_package(control, tmp_path):
+    base = tmp_path / "pk"
+    base.mkdir()
+    control.cfg["PACKAGE_DIR"] = str(base)
+    make_package(str(base), "zz-offline", 8081, 8082)  # the built-in mi355x-k8s meta claims the same ports
+    rows = {r["name"]: r for r in packages.sync_packages()}
+    assert not rows["zz-offline"]["conflict"]
+    assert "claimed by package zz-offline" in rows["mi355x-k8s"]["conflict"]
+
+
 def test_port_clash_is_refused(served):
     pkg, rp, gp, _, base = served
     make_package(str(base), "offline-z", _free_port(), gp)  # registry port of offline-a

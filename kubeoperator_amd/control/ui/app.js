@@ -454,8 +454,16 @@ views.credentials = crudPage("Credentials", "/credential/", [["Name", "name"], [
 views.packages = async (v) => {
   const rows = await GET("/packages/");
   v.innerHTML = `<h2>Offline packages</h2>${table(rows, [["Name", "name"], ["Version", (p) => esc(p.meta.version)], ["Kubernetes", (p) => esc((p.meta.vars || {}).kube_version)],
-    ["ROCm", (p) => esc((p.meta.vars || {}).rocm_version)], ["AMD device plugin", (p) => esc((p.meta.vars || {}).amd_device_plugin_image || "")], ["Path", "path"]])}`;
+    ["ROCm", (p) => esc((p.meta.vars || {}).rocm_version)], ["AMD device plugin", (p) => esc((p.meta.vars || {}).amd_device_plugin_image || "")],
+    ["Repository", (p) => endpoint(p, "repo", p.repo_port, "/repository/")], ["Registry", (p) => endpoint(p, "registry", p.registry_port, "/v2/")],
+    ["Path", "path"]])}`;
 };
+// a package endpoint: port and whether the repo service serves it (or why not: a port claimed by another package)
+function endpoint(p, kind, port, path) {
+  if (p.conflict) return `<span class="bad" title="${esc(p.conflict)}">:${esc(port)} refused</span>`;
+  const on = (p.serving || {})[kind];
+  return on ? `<span class="ok">:${esc(port)}${esc(path)}</span>` : `<span class="muted">:${esc(port)} (no content)</span>`;
+}
 
 views.regions = crudPage("Regions", "/regions/", [["Name", "name"], ["Cloud region", "cloud_region"], ["Provider", (r) => esc((r.vars || {}).provider || "")]],
   [["name", "Name"], ["cloud_region", "Cloud region"], ["template_id", "Provider template id"], ["vars", "Provider vars (JSON: provider, host/user/password …)", "json"], ["comment", "Comment"]]);

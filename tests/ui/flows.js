@@ -214,6 +214,9 @@ async function main() {
     await until(() => rowWith(new RegExp(op)) && /SUCCESS/.test($("#steps").textContent), `${label} SUCCESS`, 90000);
     return eid;
   };
+  win.location.hash = "#/packages";
+  await until(() => rowWith(/mi355x-k8s-next.*:8083.*:8084/), "package endpoints row");
+  log("package-endpoints", {row: rowWith(/mi355x-k8s-next/).textContent.replace(/\s+/g, " ").trim()});
   win.location.hash = "#/hosts";
   await until(() => $("#add") && /Register host/.test($("#view").textContent), "hosts view");
   $("#add").click();

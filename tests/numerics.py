@@ -12,6 +12,9 @@ inputs, so a tolerance means "no worse than what the framework it replaces would
 """
 from __future__ import annotations
 
+import json
+import os
+
 import torch
 
 
@@ -39,6 +42,11 @@ def check_against_bf16(name, kernel, ref, plain_bf16, factor=2.0, floor=2.0 ** -
     rows = smallest_rows(ref2, frac)
     rk, rb = row_errs(k2, ref2, rows).max().item(), row_errs(b2, ref2, rows).max().item()
     out = {"name": name, "kernel": ek, "bf16": eb, "rows_kernel": rk, "rows_bf16": rb, "rows": int(rows.numel())}
+    ev = os.environ.get("KOP_EVIDENCE_DIR")
+    if ev:  # one JSON line per check, tagged with the running test (GPU sessions keep them as evidence)
+        os.makedirs(ev, exist_ok=True)
+        with open(os.path.join(ev, "numerics_vs_bf16.jsonl"), "a") as f:
+            f.write(json.dumps({"test": os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0], **out}) + "\n")
     assert ek <= factor * eb + floor, out
     assert rk <= factor * rb + floor, out
     return out

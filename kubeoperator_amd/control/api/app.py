@@ -728,6 +728,13 @@ def create_app() -> FastAPI:
         h = _row(M.Host, hid)
         return {"job_id": jobs.submit("sync_host_info", {"host_id": h.id})}
 
+    @r.post("/host/{hid}/gpu-check/")
+    def gpu_check_host(hid: str, request: Request):
+        """Read-only GPU node check (kfd topology, rocminfo agents, amd-smi inventory) through the engine."""
+        current_user(request)
+        h = _row(M.Host, hid)
+        return hosts.check_gpu_node(h.id)
+
     @r.delete("/host/{hid}/", status_code=204)
     def delete_host(hid: str, request: Request):
         superuser(request)

@@ -14,7 +14,7 @@ with pidfiles, and the host-side ``kubeopsctl.sh``):
 Cluster operations (the UI's flows, usable headless; ``--server URL`` talks to a running control plane over
 the REST API, otherwise the store is used in-process and operations run inline with their log on stdout):
 
-    kubeopsctl host add NAME IP [--password P | --credential C] | host list | host import FILE
+    kubeopsctl host add NAME IP [--password P | --credential C] | host list | host import FILE | host gpu-check NAME
     kubeopsctl cluster create -f plan.yml        # cluster-plan YAML (name/template/package/network/storage/nodes)
     kubeopsctl cluster install|uninstall NAME [--resume]
     kubeopsctl cluster scale NAME --num N        # AUTOMATIC (IaaS) clusters
@@ -438,6 +438,19 @@ class Local:
         with open(path, "rb") as f:
             return self.hosts.import_hosts(os.path.basename(path), f.read())
 
+    def gpu_check(self, name):
+        from sqlalchemy import select
+
+        from .store import models as M
+        from .store.db import session_scope
+
+        with session_scope() as s:
+            h = s.scalar(select(M.Host).where(M.Host.name == name))
+            if h is None:
+                raise SystemExit(f"no host {name}")
+            hid = h.id
+        return self.hosts.check_gpu_node(hid)
+
     def create_cluster(self, plan_doc):
         for h in plan_doc.get("hosts") or []:
             try:
@@ -546,6 +559,12 @@ class Remote:
         with open(path, "rb") as f:
             return self._j(self.http.post("/host/import/", params={"filename": os.path.basename(path)},
                                           content=f.read()))
+
+    def gpu_check(self, name):
+        hs = [h for h in self.list_hosts() if h["name"] == name]
+        if not hs:
+            raise SystemExit(f"no host {name}")
+        return self._j(self.http.post(f"/host/{hs[0]['id']}/gpu-check/"))
 
     def create_cluster(self, plan_doc):
         for h in plan_doc.get("hosts") or []:
@@ -737,6 +756,13 @@ def cmd_host(a, cfg) -> int:
     if a.action == "import":
         print(json.dumps(b.import_hosts(a.file), indent=2))
         return 0
+    if a.action == "gpu-check":  # read-only kfd / rocminfo / amd-smi tasks of the GPU roles on that host
+        r = b.gpu_check(a.name)
+        ok = r["summary"]["success"]
+        print(f"{a.name}: {'ok' if ok else 'FAILED'} kfd GPUs={r['kfd_gpus']} rocminfo GPU agents={r['rocminfo_gpus']}")
+        if not ok:
+            print(json.dumps(r["summary"]["dark"], indent=2))
+        return 0 if ok else 1
     _table(b.list_hosts(), ["name", "ip", "status", "os", "cpu_core", "memory", "gpu_num", "gpu_info"])
     return 0
 
@@ -796,7 +822,7 @@ def main(argv=None) -> int:
     c.add_argument("--execution", help="with trace: execution id (default: the latest)")
     c.add_argument("-o", "--output", help="with trace: write the Chrome trace-event JSON here")
     h = sub.add_parser("host")
-    h.add_argument("action", choices=["add", "list", "import"])
+    h.add_argument("action", choices=["add", "list", "import", "gpu-check"])
     h.add_argument("name", nargs="?")
     h.add_argument("ip", nargs="?")
     h.add_argument("--port", type=int, default=22)

@@ -181,6 +181,15 @@ def test_host_import_multipart(client):
     assert sorted(r.json()["created"]) == ["h1", "h2"]
 
 
+def test_host_gpu_check_route(client):
+    h = client.post("/api/v1/host/", json={"name": "w1", "ip": "10.0.0.2", "password": "pw"}).json()
+    assert h["gpu_num"] == 8
+    r = client.post(f"/api/v1/host/{h['id']}/gpu-check/")
+    assert r.status_code == 200, r.text
+    d = r.json()
+    assert d["summary"]["success"] and d["kfd_gpus"] == "8" and d["rocminfo_gpus"] == "8"
+
+
 def test_messages_and_log_search(client):
     from kubeoperator_amd.control.domain import messages
     messages.insert_message({"title": "hello", "content": {"detail": "x"}}, sync=True)

@@ -204,3 +204,5 @@ def test_kubeopsctl_cluster_create_install_and_trace(tmp_path):
     import json as _json
     ev = _json.loads(out.read_text())["traceEvents"]
     assert any(e.get("cat") == "host" for e in ev) and any(e.get("cat") == "step" for e in ev)
+    r = run("host", "gpu-check", "gpu-1")  # the plan registered its hosts; gpu-1 is an 8x MI355X node of the farm
+    assert r.returncode == 0 and "gpu-1: ok" in r.stdout and "kfd GPUs=8" in r.stdout, r.stdout + r.stderr

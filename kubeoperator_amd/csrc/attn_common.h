@@ -137,6 +137,11 @@ __device__ __forceinline__ int swz(int row, int ch) {
 __device__ __forceinline__ void glds16(const void* g, char* lds_uniform) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_uniform, 16, 0, 0);
 }
+// The same with the non-temporal policy (cache-policy bits = 2, nt): for bytes one CU reads exactly once
+// (MI355X_MICROARCH.md 'nt-weights': no L2 allocation, so the re-read operands keep their lines)
+__device__ __forceinline__ void glds16_nt(const void* g, char* lds_uniform) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)lds_uniform, 16, 0, 2);
+}
 
 // Fill a swizzled [rows][ROWB] LDS image of `rows` rows by LDS-DMA: pieces of 1 KiB are spread over the
 // NW waves of the block; each lane's SOURCE chunk is permuted so the lane-linear destination is the

@@ -680,7 +680,7 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq8_kernel(
 // a causal mask) makes this kernel HBM-bound, ~3x cheaper than recomputing.
 // BLK: dS in the wave-block layout of fa_bwd_dkdv64_kernel ([B, Hq, S/32, S/64, 32 queries, 64 slots]); the
 // tile's dS rows of one head and 32-query stage are then one contiguous 4-KB block.
-template <int D, int HP, bool BLK = false>
+template <int D, int HP, bool BLK = false, bool NTL = false>
 __global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __restrict__ ds, const bf16_t* __restrict__ k,
                                                               bf16_t* __restrict__ dq, int B, int S, int Hq, int Hkv,
                                                               int64_t ks, int64_t dqs, float scale, int causal) {
@@ -721,7 +721,8 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __re
           BLK ? ds + (((int64_t)(b * Hq + hg * HP + row / RH) * (S / 32) + qrow / 32) * (S / 64) + t) * 2048 +
                     (qrow % 32) * 64 + ch * 8
               : ds + ((int64_t)(b * Hq + hg * HP + row / RH) * S + qrow) * S + t * BN + ch * 8;
-      glds16(src, sl + KT + piece * 1024);
+      if constexpr (NTL) glds16_nt(src, sl + KT + piece * 1024);  // dS: read once, by this CU only
+      else glds16(src, sl + KT + piece * 1024);
     }
   };
   issue(0);
@@ -793,18 +794,36 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __re
   }
 }
 
-template <int D, int HP, bool BLK = false>
-static void launch_dq_ds(const bf16_t* ds, const bf16_t* k, bf16_t* dq, int B, int S, int Hq, int Hkv, int64_t ks,
-                         int64_t dqs, float scale, bool causal, hipStream_t stream) {
+// dS is read exactly once, by one CU: load it non-temporally (default; KOP_DQ_NT=0 for the cached policy). The
+// K tiles every query block of the GQA group re-reads then keep their L2 lines: causal backward 1.813 / 1.826 ms vs
+// 1.886 / 1.874 ms cached, same box alternating (profiles/r4_dq_nt_ab.jsonl)
+static bool dq_nt() {
+  static const bool on = [] {
+    const char* e = getenv("KOP_DQ_NT");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return on;
+}
+
+template <int D, int HP, bool BLK, bool NTL>
+static void launch_dq_ds_nt(const bf16_t* ds, const bf16_t* k, bf16_t* dq, int B, int S, int Hq, int Hkv, int64_t ks,
+                            int64_t dqs, float scale, bool causal, hipStream_t stream) {
   const size_t lds = 3 * (64 * (D * 2) + 256 * 64 * 2);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)fa_bwd_dq_ds_kernel<D, HP, BLK>,
+    (void)hipFuncSetAttribute((const void*)fa_bwd_dq_ds_kernel<D, HP, BLK, NTL>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  fa_bwd_dq_ds_kernel<D, HP, BLK><<<B * (Hq / HP) * (S / (256 / HP)), 512, lds, stream>>>(ds, k, dq, B, S, Hq, Hkv,
-                                                                                         ks, dqs, scale, causal);
+  fa_bwd_dq_ds_kernel<D, HP, BLK, NTL><<<B * (Hq / HP) * (S / (256 / HP)), 512, lds, stream>>>(
+      ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal);
+}
+
+template <int D, int HP, bool BLK = false>
+static void launch_dq_ds(const bf16_t* ds, const bf16_t* k, bf16_t* dq, int B, int S, int Hq, int Hkv, int64_t ks,
+                         int64_t dqs, float scale, bool causal, hipStream_t stream) {
+  if (dq_nt()) launch_dq_ds_nt<D, HP, BLK, true>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+  else launch_dq_ds_nt<D, HP, BLK, false>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
 }
 
 // dk/dv = bf16(sum of the NP per-group partials): partial p of KV head h at slot h * grp + p of [T, Hq, D]

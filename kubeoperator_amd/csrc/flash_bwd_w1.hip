@@ -126,17 +126,16 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
   const float c2 = scale * 1.4426950408889634f;
   const int qt0 = causal ? k0 / BQ : 0;
   const int nqt = S / BQ;
-  // the sweep: HPW heads x nst query stages, sequence index sq -> (head hq0 + sq / nst, stage of the order below)
+  // the sweep: HPW heads x nst query stages in sequence (sq = head * nst + position in the order below). The DMA
+  // issue runs NS - 1 stages ahead through a cursor (ih, iqt) advanced one stage at a time: no integer division by
+  // the runtime stage count on the scalar unit (a first version divided per stage: +1 SALU per MFMA)
   const int nst = nqt - qt0, tot = HPW * nst;
-  auto s_qt = [&](int sq) {
-    const int i = sq % nst;
-    return REV ? nqt - 1 - i : qt0 + i;
-  };
-
-  auto issue = [&](int sq) {
-    char* base = smem + KB + (sq % NS) * STAGE;
-    const int hq = hq0 + sq / nst;
-    const int q0 = s_qt(sq) * BQ;
+  const int qfirst = REV ? nqt - 1 : qt0;
+  int ih = 0, iqt = qfirst, isq = 0;
+  auto issue_next = [&]() {
+    char* base = smem + KB + (isq % NS) * STAGE;
+    const int hq = hq0 + ih;
+    const int q0 = iqt * BQ;
     dma_tile_a<ROWB, NW, BQ>(base, q + (int64_t)(b * S + q0) * qs + hq * D, qs, wid, lane);
     dma_tile_a<ROWB, NW, BQ>(base + QT, dout + (int64_t)(b * S + q0) * dos + hq * D, dos, wid, lane);
     if (wid == 0) {
@@ -145,12 +144,18 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
       const float* src = (l < 8 ? nlse + rowh + 4 * l : ndelta + rowh + 4 * (l - 8));
       glds16(src, base + 2 * QT);
     }
+    iqt += REV ? -1 : 1;
+    if (REV ? iqt < qt0 : iqt >= nqt) {
+      ++ih;
+      iqt = qfirst;
+    }
+    ++isq;
   };
   dma_tile_a<ROWB, NW, BN>(Kl, k + (int64_t)(b * S + k0) * ks + kvh * D, ks, wid, lane);
-  issue(0);
+  issue_next();
 #pragma unroll
   for (int i = 1; i < NS - 1; ++i)
-    if (i < tot) issue(i);
+    if (isq < tot) issue_next();
 
   const int rb_lane0 = RB * (r >> 3) + 64 * (r & 7) + 16 * (hh ^ ((r >> 2) & 3));
   const int rb_lane1 = RB * (r >> 3) + 64 * (r & 7) + 16 * ((2 + hh) ^ ((r >> 2) & 3));
@@ -196,10 +201,8 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
                              : 2u * (uint32_t)((16 * (sg & 1) + si) * S + 8 * (sg >> 1));
   (void)stw0; (void)stw1; (void)str; (void)sqoff;
 
-  auto body = [&](int sq, auto mask_c) {
+  auto body = [&](int sq, int qt, uint64_t dsrow, uint64_t dsq, auto mask_c) {
     constexpr bool MASK = decltype(mask_c)::value;
-    const int qt = s_qt(sq), hq = hq0 + sq / nst;
-    const uint64_t dsrow = dsrow_of(hq), dsq = dsq_of(hq);
     (void)dsrow; (void)dsq;
     // DMA(sq) is older than: stores(sq-2), DMA(sq+NS-2), stores(sq-1) (and the other DMAs still in flight)
     int younger = st1 + st2;
@@ -211,7 +214,7 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     if constexpr (!(DIAG & 8)) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if constexpr (!(DIAG & 4)) {
-      if (sq + NS - 1 < tot) issue(sq + NS - 1);
+      if (isq < tot) issue_next();  // the cursor is at stage sq + NS - 1
     }
     const int qs0 = qt * BQ;
     if (causal && qs0 + BQ - 1 < k0w) return;  // every query of the stage precedes every key of the wave
@@ -441,13 +444,14 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
   // made hipcc spill ~500 VGPRs
   for (int hi = 0; hi < HPW; ++hi) {
     const int s0 = hi * nst;
+    const uint64_t dr = dsrow_of(hq0 + hi), dq = dsq_of(hq0 + hi);
     if constexpr (REV) {
-      for (int qt = nqt - 1; qt >= qd; --qt) body(s0 + (nqt - 1 - qt), std::false_type{});
-      for (int qt = qd - 1; qt >= qt0; --qt) body(s0 + (nqt - 1 - qt), std::true_type{});
+      for (int qt = nqt - 1; qt >= qd; --qt) body(s0 + (nqt - 1 - qt), qt, dr, dq, std::false_type{});
+      for (int qt = qd - 1; qt >= qt0; --qt) body(s0 + (nqt - 1 - qt), qt, dr, dq, std::true_type{});
     } else {
       int qt = qt0;
-      for (; qt < qd; ++qt) body(s0 + (qt - qt0), std::true_type{});
-      for (; qt < nqt; ++qt) body(s0 + (qt - qt0), std::false_type{});
+      for (; qt < qd; ++qt) body(s0 + (qt - qt0), qt, dr, dq, std::true_type{});
+      for (; qt < nqt; ++qt) body(s0 + (qt - qt0), qt, dr, dq, std::false_type{});
     }
   }
   // the accumulators leave the AGPRs through compiler v_accvgpr_read: 18 wait states after the last 16-pass MFMA

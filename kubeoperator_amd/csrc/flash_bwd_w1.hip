@@ -127,29 +127,39 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
   const int qt0 = causal ? k0 / BQ : 0;
   const int nqt = S / BQ;
   // the sweep: HPW heads x nst query stages in sequence (sq = head * nst + position in the order below). The DMA
-  // issue runs NS - 1 stages ahead through a cursor (ih, iqt) advanced one stage at a time: no integer division by
-  // the runtime stage count on the scalar unit (a first version divided per stage: +1 SALU per MFMA)
+  // issue runs NS - 1 stages ahead through a cursor advanced one stage at a time: the Q / dO / lse-delta source
+  // pointers step by +-BQ rows (and jump to the next head's first stage at the end of a head), the ring slot is a
+  // counter -- no integer multiply or division on the scalar unit per stage (the per-stage address products and
+  // `% NS` were ~70 serial instructions in front of every stage's first MFMA)
   const int nst = nqt - qt0, tot = HPW * nst;
   const int qfirst = REV ? nqt - 1 : qt0;
-  int ih = 0, iqt = qfirst, isq = 0;
+  constexpr int QSTEP = REV ? -BQ : BQ;
+  int iqt = qfirst, isq = 0, islot = 0;
+  const bf16_t* iq = q + (int64_t)(b * S + qfirst * BQ) * qs + hq0 * D;
+  const bf16_t* io = dout + (int64_t)(b * S + qfirst * BQ) * dos + hq0 * D;
+  const int64_t iq_step = (int64_t)QSTEP * qs, io_step = (int64_t)QSTEP * dos;
+  const int64_t iq_wrap = D - (int64_t)nst * iq_step, io_wrap = D - (int64_t)nst * io_step;
+  // lse / delta rows of the stage: lane l < 8 reads -lse/scale floats 4l.., lanes 8..15 -delta floats 4(l-8)..
+  const float* il = (((lane & 15) < 8) ? nlse + 4 * (lane & 15) : ndelta + 4 * ((lane & 15) - 8)) +
+                    ((int64_t)(b * Hq + hq0)) * S + qfirst * BQ;
+  const int64_t il_wrap = S - (int64_t)nst * QSTEP;
   auto issue_next = [&]() {
-    char* base = smem + KB + (isq % NS) * STAGE;
-    const int hq = hq0 + ih;
-    const int q0 = iqt * BQ;
-    dma_tile_a<ROWB, NW, BQ>(base, q + (int64_t)(b * S + q0) * qs + hq * D, qs, wid, lane);
-    dma_tile_a<ROWB, NW, BQ>(base + QT, dout + (int64_t)(b * S + q0) * dos + hq * D, dos, wid, lane);
-    if (wid == 0) {
-      const int l = lane & 15;
-      const int64_t rowh = ((int64_t)(b * Hq + hq)) * S + q0;
-      const float* src = (l < 8 ? nlse + rowh + 4 * l : ndelta + rowh + 4 * (l - 8));
-      glds16(src, base + 2 * QT);
-    }
+    char* base = smem + KB + islot * STAGE;
+    dma_tile_a<ROWB, NW, BQ>(base, iq, qs, wid, lane);
+    dma_tile_a<ROWB, NW, BQ>(base + QT, io, dos, wid, lane);
+    if (wid == 0) glds16(il, base + 2 * QT);
     iqt += REV ? -1 : 1;
+    iq += iq_step;
+    io += io_step;
+    il += QSTEP;
     if (REV ? iqt < qt0 : iqt >= nqt) {
-      ++ih;
       iqt = qfirst;
+      iq += iq_wrap;
+      io += io_wrap;
+      il += il_wrap;
     }
     ++isq;
+    islot = islot == NS - 1 ? 0 : islot + 1;
   };
   dma_tile_a<ROWB, NW, BN>(Kl, k + (int64_t)(b * S + k0) * ks + kvh * D, ks, wid, lane);
   issue_next();
@@ -201,16 +211,24 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
                              : 2u * (uint32_t)((16 * (sg & 1) + si) * S + 8 * (sg >> 1));
   (void)stw0; (void)stw1; (void)str; (void)sqoff;
 
+  int cslot = 0;  // ring slot of the stage being computed (sq % NS)
   auto body = [&](int sq, int qt, uint64_t dsrow, uint64_t dsq, auto mask_c) {
     constexpr bool MASK = decltype(mask_c)::value;
     (void)dsrow; (void)dsq;
-    // DMA(sq) is older than: stores(sq-2), DMA(sq+NS-2), stores(sq-1) (and the other DMAs still in flight)
-    int younger = st1 + st2;
-#pragma unroll
-    for (int i = 1; i < NS - 1; ++i) younger += (sq + i < tot) ? pcount : 0;
-    if constexpr (!(DIAG & 36)) vm_wait_le(younger);
+    // DMA(sq) is older than: stores(sq-2), DMA(sq+NS-2), stores(sq-1) (and the other DMAs still in flight). In the
+    // steady state that is 8 + MYP (+1 on wave 0, whose lse/delta piece the constant wait then also retires: a
+    // stricter wait, still correct); a runtime count goes through vm_wait_le's compare tree (~45 scalar
+    // instructions and 16 branches), so only the sweep's first stages and its tail take it
+    if constexpr (!(DIAG & 36)) {
+      static_assert(NS == 3 && 8 + MYP <= 15, "constant steady-state wait");
+      const int younger = st1 + st2 + ((sq + 1 < tot) ? pcount : 0);
+      if (younger >= 8 + MYP) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + MYP) : "memory");
+      else vm_wait_le(younger);
+    }
     st2 = st1;
     st1 = 0;
+    const int slot = cslot;
+    cslot = cslot == NS - 1 ? 0 : cslot + 1;
     if constexpr (!(DIAG & 8)) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if constexpr (!(DIAG & 4)) {
@@ -218,7 +236,7 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     }
     const int qs0 = qt * BQ;
     if (causal && qs0 + BQ - 1 < k0w) return;  // every query of the stage precedes every key of the wave
-    const char* Ql = smem + KB + (sq % NS) * STAGE;
+    const char* Ql = smem + KB + slot * STAGE;
     const char* Ol = Ql + QT;
     // Every LDS read below is an inline-asm read retired by a counted lgkmcnt, and every step ends in
     // sched_barrier(0): left to itself hipcc sank the MFMAs below later reads, which serialised them (one wave

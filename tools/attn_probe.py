@@ -50,14 +50,16 @@ def main():
         do = torch.randn_like(o)
         dqkv = torch.empty_like(qkv)
         ws = torch.empty(lib.flash_attn_bwd_workspace(B, S, Hq, D), dtype=torch.uint8, device="cuda")
+        ot = torch.empty(Hq * D, B * S, device="cuda", dtype=torch.bfloat16)  # O^T companion (the training step's form)
         sc = 1 / math.sqrt(D)
         for causal in [bool(int(x)) for x in a.causal.split(",")]:
             fl = 4 * B * Hq * S * S * D * (0.5 if causal else 1.0)
             tf = timeit(lambda: lib.flash_attn_fwd(q, k, v, o, lse, B, S, Hq, Hkv, D, sc, causal), a.iters)
+            tft = timeit(lambda: lib.flash_attn_fwd_t(q, k, v, o, ot, lse, B, S, Hq, Hkv, D, sc, causal), a.iters)
             tb = timeit(lambda: lib.flash_attn_bwd(q, k, v, o, do, lse, dqkv[:, :x], dqkv[:, x:c], dqkv[:, c:], ws,
                                                    B, S, Hq, Hkv, D, sc, causal), max(3, a.iters // 2))
             print(json.dumps({"tag": a.tag, "shape": name, "causal": causal, "fwd_ms": round(tf, 4),
-                              "fwd_tflops": round(fl / tf / 1e9, 1), "bwd_ms": round(tb, 4),
+                              "fwd_tflops": round(fl / tf / 1e9, 1), "fwd_ot_ms": round(tft, 4), "bwd_ms": round(tb, 4),
                               "bwd_tflops": round(2.5 * fl / tb / 1e9, 1)}), flush=True)
 
 

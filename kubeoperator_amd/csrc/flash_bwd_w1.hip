@@ -518,12 +518,19 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
 
 // heads per workgroup: the largest power of two dividing the GQA group that still leaves >= 2 workgroups per CU
 // (the causal key blocks differ 32x in work; fewer, longer workgroups would end on a few heavy ones).
-// KOP_DKDV_HPW overrides (1 / 2 / 4 / 8).
-static int pick_hpw(int B, int S, int Hq, int Hkv) {
-  static const int env = [] {
+// KOP_DKDV_HPW / flash_attn_set_dkdv_hpw override it (1 / 2 / 4 / 8; 0 automatic).
+static int g_hpw = -1;  // -1: read KOP_DKDV_HPW on first use; 0: automatic; 1 / 2 / 4 / 8: forced
+int flash_attn_set_dkdv_hpw(int h) {
+  if (g_hpw < 0) {
     const char* e = getenv("KOP_DKDV_HPW");
-    return e ? atoi(e) : 0;
-  }();
+    g_hpw = e ? atoi(e) : 0;
+  }
+  const int old = g_hpw;
+  if (h >= 0) g_hpw = h;
+  return old;
+}
+static int pick_hpw(int B, int S, int Hq, int Hkv) {
+  const int env = flash_attn_set_dkdv_hpw(-1);
   const int grp = Hq / Hkv;
   if (env > 0) return (grp % env == 0 && env <= 8) ? env : 1;
   static int cus = 0;

@@ -76,6 +76,8 @@ size_t flash_attn_bwd_workspace(int B, int S, int Hq, int D);
 // v < 0 only queries; returns the previous value. The workspace size depends on it.
 int flash_attn_set_dq_variant(int v);
 int flash_attn_set_dkdv_cfg(int c);
+// heads per workgroup of the one-wave dK/dV kernel: 0 automatic, 1 / 2 / 4 / 8 forced; h < 0 only reads it
+int flash_attn_set_dkdv_hpw(int h);
 // forward kernel variant: -1 per-head-dim default, 8 / 9 / 10 the 8-wave kernel, < 8 the 4-wave kernel; returns the old
 // setting (an argument below -1 only reads it)
 int flash_attn_set_fwd_variant(int v);

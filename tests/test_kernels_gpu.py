@@ -393,6 +393,46 @@ def test_flash_attention_bwd_dq_variants(variant, cfg, D, Hq, Hkv, S, causal):
         lib().flash_attn_set_dkdv_cfg(old_cfg)
 
 
+@pytest.mark.parametrize("hpw", [2, 4, 8])
+@pytest.mark.parametrize("D,cfg,B,S,Hq,Hkv", [(128, 64, 1, 768, 8, 2), (128, 64, 2, 512, 8, 1), (128, 64, 1, 1024, 16, 2),
+                                              (64, 640, 1, 512, 8, 1)])
+@pytest.mark.parametrize("causal", [True, False])
+def test_dkdv_head_sweep_matches_one_head_per_workgroup(hpw, D, cfg, B, S, Hq, Hkv, causal):
+    """The one-wave dK/dV kernel sweeping HPW query heads of a GQA group per workgroup (csrc/flash_bwd_w1.hip: the
+    issue cursor steps through the heads' stages and wraps to the next head; HPW == the group size writes bf16 dK / dV
+    directly, fewer heads leave grp / HPW fp32 partials for the finalize pass). The test shapes are too small for the
+    automatic choice to pick HPW > 1, so it is forced: gradients against the fp32 reference and against HPW 1."""
+    from kubeoperator_amd.ops.functional import rope_attention
+    from kubeoperator_amd.ops.reference import attention_ref
+
+    if (Hq // Hkv) % hpw:
+        pytest.skip("HPW must divide the GQA group")
+    old_cfg = lib().flash_attn_set_dkdv_cfg(cfg)
+    old_hpw = lib().flash_attn_set_dkdv_hpw(1)
+    try:
+        torch.manual_seed(13)
+        qkv0 = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
+        do = torch.randn(B * S, Hq * D, device=DEV, dtype=torch.bfloat16)
+        grads = {}
+        for h in (1, hpw):
+            lib().flash_attn_set_dkdv_hpw(h)
+            qkv = qkv0.clone().requires_grad_(True)
+            o = rope_attention(qkv, None, None, B, S, Hq, Hkv, D, causal=causal, use_rope=False)
+            (o.float() * do.float()).sum().backward()
+            grads[h] = qkv.grad.float()
+        x = qkv0.float().requires_grad_(True)
+        a, c = Hq * D, (Hq + Hkv) * D
+        of, _ = attention_ref(x[:, :a], x[:, a:c], x[:, c:], B, S, Hq, Hkv, D, causal)
+        (of * do.float()).sum().backward()
+        for lo, hi in ((0, a), (a, c), (c, x.shape[1])):
+            assert rel_err(grads[hpw][:, lo:hi], x.grad[:, lo:hi]) < 3e-2
+            # same products, another fp32 summation order of the heads (registers vs partials): bf16-rounding close
+            assert rel_err(grads[hpw][:, lo:hi], grads[1][:, lo:hi]) < 1e-2
+    finally:
+        lib().flash_attn_set_dkdv_cfg(old_cfg)
+        lib().flash_attn_set_dkdv_hpw(old_hpw)
+
+
 @pytest.mark.parametrize("rows,H", [(8192, 768), (8192, 2304), (4096, 3072), (77, 24), (1000, 1024)])
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_bias_grad_matches_reference(rows, H, accumulate):

@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
   constexpr int DT = D / 32, NK = D / 16, RB = ROWB * 8;
   static_assert(NS == 3, "the vmcnt bookkeeping below tracks the stores of the two previous stages");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* const Kl = smem;
+  char* const Kl = smem;  // K image of the workgroup's 256 keys: only the second 32-key block of each wave is read
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -143,6 +143,7 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
   const float* il = (((lane & 15) < 8) ? nlse + 4 * (lane & 15) : ndelta + 4 * ((lane & 15) - 8)) +
                     ((int64_t)(b * Hq + hq0)) * S + qfirst * BQ;
   const int64_t il_wrap = S - (int64_t)nst * QSTEP;
+  dma_tile_a<ROWB, NW, BN>(Kl, k + (int64_t)(b * S + k0) * ks + kvh * D, ks, wid, lane);
   auto issue_next = [&]() {
     char* base = smem + KB + islot * STAGE;
     dma_tile_a<ROWB, NW, BQ>(base, iq, qs, wid, lane);
@@ -161,7 +162,6 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     ++isq;
     islot = islot == NS - 1 ? 0 : islot + 1;
   };
-  dma_tile_a<ROWB, NW, BN>(Kl, k + (int64_t)(b * S + k0) * ks + kvh * D, ks, wid, lane);
   issue_next();
 #pragma unroll
   for (int i = 1; i < NS - 1; ++i)
@@ -172,17 +172,23 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
   const int tb_lane0 = 64 * (4 * hh + tq) + 16 * ((2 * tg1 + (tp >> 1)) ^ hh) + 8 * (tp & 1);
   const int tb_lane1 = 64 * (4 * hh + tq) + 16 * ((2 * tg1 + (tp >> 1)) ^ (2 + hh)) + 8 * (tp & 1);
 
-  // V^T fragments of the wave's 64 keys (B operand of dP = dO.V^T; key = k0w + 32*c + r), resident
-  bf16x8 vf0[NK], vf1[NK];
+  // V^T fragments (B operand of dP = dO.V^T) of the wave's 64 keys and the K^T fragments (B operand of S = Q.K^T)
+  // of its first 32 keys (key = k0w + 32*c + r, columns 16kk + 8hh ..), resident for the whole sweep; the second
+  // key block's K rows still come from the LDS image. (Every stage used to re-read all 64 keys' K rows from LDS: 16
+  // of the ~56 KB a wave read per stage, with the stage LDS-bandwidth bound -- dropping the 8 KB of dS staging
+  // traffic alone saved 14 %. All 64 keys resident spilled at 512 registers and ran 11 % slower: r4_experiments.md.)
+  bf16x8 vf0[NK], vf1[NK], kf0[NK];
   {
     const bf16_t* vp = v + (int64_t)(b * S + k0w + r) * vs + kvh * D + 8 * hh;
+    const bf16_t* kp = k + (int64_t)(b * S + k0w + r) * ks + kvh * D + 8 * hh;
 #pragma unroll
     for (int kk = 0; kk < NK; ++kk) {
       vf0[kk] = *reinterpret_cast<const bf16x8*>(vp + 16 * kk);
       vf1[kk] = *reinterpret_cast<const bf16x8*>(vp + 32 * vs + 16 * kk);
+      kf0[kk] = *reinterpret_cast<const bf16x8*>(kp + 16 * kk);
     }
 #pragma unroll
-    for (int kk = 0; kk < NK; ++kk) asm volatile("" : "+v"(vf0[kk]), "+v"(vf1[kk]));
+    for (int kk = 0; kk < NK; ++kk) asm volatile("" : "+v"(vf0[kk]), "+v"(vf1[kk]), "+v"(kf0[kk]));
   }
   f32x16 dk0[DT], dk1[DT], dv0[DT], dv1[DT];
 #pragma unroll
@@ -244,17 +250,16 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     // of a step, 128 cycles) for transposed reads.
     const uint32_t qb0 = lds_addr(Ql) + rb_lane0, qb1 = lds_addr(Ql) + rb_lane1;
     const uint32_t ob0 = lds_addr(Ol) + rb_lane0, ob1 = lds_addr(Ol) + rb_lane1;
-    const uint32_t kw0 = lds_addr(Kl) + rb_lane0 + RB * 8 * wid, kw1 = lds_addr(Kl) + rb_lane1 + RB * 8 * wid;
+    const uint32_t kw0 = lds_addr(Kl) + rb_lane0 + RB * 8 * wid + RB * 4, kw1 = lds_addr(Kl) + rb_lane1 + RB * 8 * wid + RB * 4;
     const uint32_t o0 = lds_addr(Ol) + tb_lane0, o1 = lds_addr(Ol) + tb_lane1;
     const uint32_t qa0 = lds_addr(Ql) + tb_lane0, qa1 = lds_addr(Ql) + tb_lane1;
     // -lse/scale (bytes 0..127) and -delta (128..255) of the stage's queries; accumulator row j is query
     // (j&3) + 8(j>>2) + 4hh, i.e. floats 8g + 4hh .. +3 for register quad g
     const uint32_t ldb = lds_addr(Ql + 2 * QT) + 16 * hh;
-    auto grp = [&](auto kc, bf16x8* d3) {  // S-phase row reads of k-step kk: Q row, K rows of both key blocks
+    auto grp = [&](auto kc, bf16x8* d2) {  // S-phase row reads of k-step kk: the Q row, the second key block's K row
       constexpr int kk = decltype(kc)::value;
-      d3[0] = lds_read8_off<512 * (kk >> 1)>((kk & 1) ? qb1 : qb0);
-      d3[1] = lds_read8_off<512 * (kk >> 1)>((kk & 1) ? kw1 : kw0);
-      d3[2] = lds_read8_off<RB * 4 + 512 * (kk >> 1)>((kk & 1) ? kw1 : kw0);
+      d2[0] = lds_read8_off<512 * (kk >> 1)>((kk & 1) ? qb1 : qb0);
+      d2[1] = lds_read8_off<512 * (kk >> 1)>((kk & 1) ? kw1 : kw0);
     };
     auto dor = [&](auto kc) {  // dP-phase row read of k-step kk: dO row
       constexpr int kk = decltype(kc)::value;
@@ -272,11 +277,11 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     // ---- S = Q.K^T (16 MFMAs); the -lse/scale C operand is shared by both key blocks
     f32x4 lq[4];
     static_for<4>([&](auto g) { lq[decltype(g)::value] = lds_read16f_off<32 * decltype(g)::value>(ldb); });
-    bf16x8 ga[3], gb[3], gc[3];
+    bf16x8 ga[2], gb[2], gc[2];
     grp(std::integral_constant<int, 0>{}, ga);
     grp(std::integral_constant<int, 1>{}, gb);
     grp(std::integral_constant<int, 2>{}, gc);
-    asm volatile("s_waitcnt lgkmcnt(9)" : "+v"(lq[0]), "+v"(lq[1]), "+v"(lq[2]), "+v"(lq[3]));
+    asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(lq[0]), "+v"(lq[1]), "+v"(lq[2]), "+v"(lq[3]));
     const f32x16 cl = cat4f(lq);
     f32x16 s0, s1;
     bf16x8 dof[3];
@@ -285,10 +290,10 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
       constexpr int kk = decltype(kc)::value;
       bf16x8* cur = (kk % 3 == 0) ? ga : (kk % 3 == 1) ? gb : gc;
       // younger than group kk: the next two groups, and from step NK-2 on the dP phase's 7 early reads
-      constexpr int younger = 3 * (NK - 1 - kk < 2 ? NK - 1 - kk : 2) + (kk > NK - 3 ? 7 : 0);
-      wait_rows3<younger>(cur);
-      s0 = mfma32(cur[0], cur[1], kk == 0 ? cl : s0);
-      s1 = mfma32(cur[0], cur[2], kk == 0 ? cl : s1);
+      constexpr int younger = 2 * (NK - 1 - kk < 2 ? NK - 1 - kk : 2) + (kk > NK - 3 ? 7 : 0);
+      asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(cur[0]), "+v"(cur[1]) : "n"(younger));
+      s0 = mfma32(cur[0], kf0[kk], kk == 0 ? cl : s0);
+      s1 = mfma32(cur[0], cur[1], kk == 0 ? cl : s1);
       if constexpr (kk + 3 < NK) grp(std::integral_constant<int, kk + 3>{}, cur);
       if constexpr (kk == NK - 3) {  // the dP phase's first reads fly under the last S MFMAs
         static_for<4>([&](auto g) { ld[decltype(g)::value] = lds_read16f_off<128 + 32 * decltype(g)::value>(ldb); });

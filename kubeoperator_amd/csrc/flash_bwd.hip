@@ -680,7 +680,11 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq8_kernel(
 // a causal mask) makes this kernel HBM-bound, ~3x cheaper than recomputing.
 // BLK: dS in the wave-block layout of fa_bwd_dkdv64_kernel ([B, Hq, S/32, S/64, 32 queries, 64 slots]); the
 // tile's dS rows of one head and 32-query stage are then one contiguous 4-KB block.
-template <int D, int HP, bool BLK = false, bool NTL = false>
+// KMAJ: dS in the key-major tiles of fa_bwd_dkdv64_kernel<QM = false, BLK> ([B, Hq, S/64, S/32, 64 keys, 32 queries]):
+// each wave's 32 query rows of a 64-key tile are one such 4-KB tile, copied lane-linear into LDS and read with
+// ds_read_b64_tr_b16 (rows = keys 64 B apart: one 32-lane half reads 4 consecutive rows, 256 B, conflict-free); the
+// two transposed reads of a k-step take keys R0 + 4hh + 0..3 and R0 + 8 + 4hh + 0..3, the k order of the K^T operand.
+template <int D, int HP, bool BLK = false, bool NTL = false, bool KMAJ = false>
 __global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __restrict__ ds, const bf16_t* __restrict__ k,
                                                               bf16_t* __restrict__ dq, int B, int S, int Hq, int Hkv,
                                                               int64_t ks, int64_t dqs, float scale, int causal) {
@@ -714,6 +718,14 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __re
 #pragma unroll
     for (int i = 0; i < (DST / 1024) / NW; ++i) {
       const int piece = wid + i * NW;
+      if constexpr (KMAJ) {  // piece = 1 KB of image tile piece / 4 (= rows 32 * tile ..), lane-linear
+        const int tile = piece >> 2, sub = piece & 3;
+        const bf16_t* src = ds + (((int64_t)(b * Hq + hg * HP + (32 * tile) / RH) * (S / 64) + t) * (S / 32) +
+                                  (q0 + (32 * tile) % RH) / 32) * 2048 + sub * 512 + lane * 8;
+        if constexpr (NTL) glds16_nt(src, sl + KT + piece * 1024);
+        else glds16(src, sl + KT + piece * 1024);
+        continue;
+      }
       const int row = 8 * piece + lrow;
       const int ch = 4 * lhi + (lslot ^ ((row >> 2) & 3));
       const int qrow = q0 + row % RH;
@@ -735,6 +747,9 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __re
   // dS row reads of image row 32*wid + r at chunk 2*ks4 + hh in the sub-tiled [256][128 B] image
   const int ds_lane0 = 4096 * wid + 1024 * (r >> 3) + 64 * (r & 7) + 16 * (hh ^ ((r >> 2) & 3));
   const int ds_lane1 = 4096 * wid + 1024 * (r >> 3) + 64 * (r & 7) + 16 * ((2 + hh) ^ ((r >> 2) & 3));
+  // KMAJ transposed reads of the wave's [64 keys][32 queries] tile: lane 4q + p of its 16-lane group gives row (key)
+  // R0 + 4hh + q, queries 16 tg1 + 4p .. +3
+  const int dk_lane = 4096 * wid + 64 * (4 * hh + tq) + 32 * tg1 + 8 * tp;
   f32x16 acc[DT];
 #pragma unroll
   for (int i = 0; i < DT; ++i) acc[i] = f32x16{0};
@@ -752,9 +767,14 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __re
       const uint32_t kb0 = lds_addr(sl) + kb_lane0, kb1 = lds_addr(sl) + kb_lane1;
       const uint32_t db0 = lds_addr(sl + KT) + ds_lane0, db1 = lds_addr(sl + KT) + ds_lane1;
       bf16x8 f[4];
+      const uint32_t dk0 = lds_addr(sl + KT) + dk_lane;
+      (void)dk0;
       static_for<4>([&](auto ks4c) {
         constexpr int ks4 = decltype(ks4c)::value;
-        f[ks4] = lds_read8_off<512 * (ks4 >> 1)>((ks4 & 1) ? db1 : db0);
+        if constexpr (KMAJ)
+          f[ks4] = cat44(lds_tr_read_off<1024 * ks4>(dk0), lds_tr_read_off<1024 * ks4 + 512>(dk0));
+        else
+          f[ks4] = lds_read8_off<512 * (ks4 >> 1)>((ks4 & 1) ? db1 : db0);
       });
       const bool diag = causal && kv0 + BN - 1 > q0w;
       static_for<4>([&](auto ks4c) {
@@ -805,25 +825,25 @@ static bool dq_nt() {
   return on;
 }
 
-template <int D, int HP, bool BLK, bool NTL>
+template <int D, int HP, bool BLK, bool NTL, bool KMAJ = false>
 static void launch_dq_ds_nt(const bf16_t* ds, const bf16_t* k, bf16_t* dq, int B, int S, int Hq, int Hkv, int64_t ks,
                             int64_t dqs, float scale, bool causal, hipStream_t stream) {
   const size_t lds = 3 * (64 * (D * 2) + 256 * 64 * 2);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)fa_bwd_dq_ds_kernel<D, HP, BLK, NTL>,
+    (void)hipFuncSetAttribute((const void*)fa_bwd_dq_ds_kernel<D, HP, BLK, NTL, KMAJ>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  fa_bwd_dq_ds_kernel<D, HP, BLK, NTL><<<B * (Hq / HP) * (S / (256 / HP)), 512, lds, stream>>>(
+  fa_bwd_dq_ds_kernel<D, HP, BLK, NTL, KMAJ><<<B * (Hq / HP) * (S / (256 / HP)), 512, lds, stream>>>(
       ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal);
 }
 
-template <int D, int HP, bool BLK = false>
+template <int D, int HP, bool BLK = false, bool KMAJ = false>
 static void launch_dq_ds(const bf16_t* ds, const bf16_t* k, bf16_t* dq, int B, int S, int Hq, int Hkv, int64_t ks,
                          int64_t dqs, float scale, bool causal, hipStream_t stream) {
-  if (dq_nt()) launch_dq_ds_nt<D, HP, BLK, true>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-  else launch_dq_ds_nt<D, HP, BLK, false>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+  if (dq_nt()) launch_dq_ds_nt<D, HP, BLK, true, KMAJ>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+  else launch_dq_ds_nt<D, HP, BLK, false, KMAJ>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
 }
 
 // dk/dv = bf16(sum of the NP per-group partials): partial p of KV head h at slot h * grp + p of [T, Hq, D]
@@ -913,22 +933,24 @@ static void launch_dkdv_ds(const bf16_t* q, const bf16_t* k, const bf16_t* v, co
 
 // dQ from the materialised dS with HP q-heads of a GQA group per workgroup (HP the largest power of two <= 8
 // dividing the group)
-template <int D, bool BLK>
+template <int D, bool BLK, bool KMAJ = false>
 static void launch_dq_ds_hp(int hp, const bf16_t* ds, const bf16_t* k, bf16_t* dq, int B, int S, int Hq, int Hkv,
                             int64_t ks, int64_t dqs, float scale, bool causal, hipStream_t stream) {
-  if (hp == 8) launch_dq_ds<D, 8, BLK>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-  else if (hp == 4) launch_dq_ds<D, 4, BLK>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-  else if (hp == 2) launch_dq_ds<D, 2, BLK>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
-  else launch_dq_ds<D, 1, BLK>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+  if (hp == 8) launch_dq_ds<D, 8, BLK, KMAJ>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+  else if (hp == 4) launch_dq_ds<D, 4, BLK, KMAJ>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+  else if (hp == 2) launch_dq_ds<D, 2, BLK, KMAJ>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+  else launch_dq_ds<D, 1, BLK, KMAJ>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
 }
 
 static int g_dkdv_cfg = -1;  // -1: read KOP_DKDV_CFG on first use
 static int dkdv_cfg() {
   if (g_dkdv_cfg < 0) {
-    // 64: one wave per SIMD, 64 keys per wave, wave-block dS (D = 128); 66: the same with row-major dS; 42: two
-    // waves per SIMD (every D); 83 / 82: 8-wave workgroups with a 3- / 2-deep stage ring (D = 128)
+    // 67 (default): one wave per SIMD, 64 keys per wave, key-major dS tiles stored from registers (D = 128); 64: the
+    // same with the LDS-staged wave-block dS; 66: LDS-staged row-major dS; 42: two waves per SIMD (every D); 83 / 82:
+    // 8-wave workgroups with a 3- / 2-deep stage ring (D = 128). 67 vs 64: causal backward 1.731 / 1.721 ms vs
+    // 1.778 / 1.790 ms at the Llama-3-8B shape, same box (profiles/r4_dkdv_kmaj_ab.jsonl)
     const char* e = getenv("KOP_DKDV_CFG");
-    g_dkdv_cfg = e ? atoi(e) : 64;
+    g_dkdv_cfg = e ? atoi(e) : 67;
   }
   return g_dkdv_cfg;
 }
@@ -976,14 +998,17 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
     const int grp = Hq / Hkv;  // heads per dQ workgroup: largest power of two dividing the GQA group, <= 8
     const int hp = (grp % 8 == 0) ? 8 : (grp % 4 == 0) ? 4 : (grp % 2 == 0) ? 2 : 1;
     // one wave per SIMD (flash_bwd_w1.hip): query-major dS staged through LDS into whole-line stores, in the
-    // wave-block layout (cfg 64; 640 = the same at D = 64, opt-in) or plain rows (66)
-    const bool one_wave = S % 256 == 0 && ((D == 128 && (cfg == 64 || cfg == 66)) || (D == 64 && cfg == 640));
+    // wave-block layout (cfg 64; 640 = the same at D = 64, opt-in) or plain rows (66); cfg 67 / 670: key-major tiles
+    // stored straight from the accumulators (no LDS staging), read back transposed by the dQ kernel
+    const bool kmaj = (D == 128 && cfg == 67) || (D == 64 && cfg == 670);
+    const bool one_wave = S % 256 == 0 && ((D == 128 && (cfg == 64 || cfg == 66 || cfg == 67)) ||
+                                           (D == 64 && (cfg == 640 || cfg == 670)));
     const bool blk = one_wave && cfg != 66;
     bool done = false;
     int np = direct ? 0 : Hq / Hkv;  // fp32 partials per GQA group left for the finalize pass
     if (one_wave) {
       np = flash_attn_bwd_dkdv64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, D, qs, ks, vs,
-                                 dos, dks, dvs, scale, cflag, true, blk, stream);
+                                 dos, dks, dvs, scale, cflag, !kmaj, blk, stream);
       done = true;
     }
     if constexpr (D == 128) {
@@ -1001,13 +1026,14 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
     if (!done)
       launch_dkdv_ds<D, NW, 2>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs,
                                dos, dks, dvs, scale, cflag, stream);
-    if (blk) launch_dq_ds_hp<D, true>(hp, ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+    if (one_wave && kmaj) launch_dq_ds_hp<D, false, true>(hp, ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+    else if (blk) launch_dq_ds_hp<D, true>(hp, ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
     else launch_dq_ds_hp<D, false>(hp, ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
     if (np > 0) fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs, np);
     return;
   }
   int np = Hq / Hkv;
-  if (D == 128 && dkdv_cfg() == 64 && S % 256 == 0) {
+  if (D == 128 && (dkdv_cfg() == 64 || dkdv_cfg() == 67) && S % 256 == 0) {
     // the one-wave dK/dV kernel without dS stores; dQ recomputes S and dP below. It writes bf16 dK / dV itself
     // when Hq == Hkv, so the finalize pass is then skipped.
     np = flash_attn_bwd_dkdv64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, nullptr, B, S, Hq, Hkv, D, qs, ks,

@@ -91,6 +91,12 @@ __device__ __forceinline__ void vm_wait_le(int n) {
 // stored straight from the accumulators, measured slower and is no longer launched: profiles/r3_experiments.md.)
 // BLK (with QM): wave-block dS layout [B, Hq, S/32, S/64, 32 queries, 64 slots]: a wave's stage tile is one contiguous
 // 4 KB block (its workgroup's stage: 16 KB), instead of 32 rows of 128 B spread 2*S bytes apart.
+// KT (QM = false with BLK): key-major tiles [B, Hq, S/64, S/32, 64 keys, 32 queries], natural key and query order: a
+// wave's stage tile is again one contiguous 4 KB block, but stored straight from the accumulators (one
+// v_permlane32_swap per dword pairs the lane halves into 8-query runs; 4 dwordx4 stores whose partial lines all come
+// from this wave in this stage and merge in L2) -- no LDS staging. The stage is LDS-bandwidth bound and the staging
+// was 8 of the ~48 KB a wave moves through LDS per stage (profiles/r4_experiments.md); fa_bwd_dq_ds_kernel<KT> reads
+// the tiles back with ds_read_b64_tr_b16.
 // REV: sweep the query stages from the last one down to the workgroup's diagonal. Every workgroup of a head then
 // reads the same Q / dO stage at the same time (forward order starts workgroup kb 8*kb stages later, so a stage is
 // re-read ~16 us apart -- long enough for the dS write stream to evict it from the XCD's 4 MB L2).
@@ -197,8 +203,12 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
   const int pcount = MYP + (wid == 0 ? 1 : 0);  // DMA ops this wave issues per stage
   int st1 = 0, st2 = 0;                           // dS stores issued in the previous / second-previous stage
   // dS^T rows of the wave's keys: row pointer in SGPRs (per head), lane offset (key r, queries 16s + 8hh) in one VGPR
-  auto dsrow_of = [&](int hq) { return (uint64_t)(uintptr_t)(dst + ((int64_t)(b * Hq + hq) * S + k0w) * S); };
-  const uint32_t dsoff = 2u * (uint32_t)(r * S + 8 * hh);
+  constexpr bool KT = !QM && BLK;
+  auto dsrow_of = [&](int hq) {
+    return KT ? (uint64_t)(uintptr_t)(dst + (((int64_t)(b * Hq + hq) * (S / 64) + k0w / 64) * (S / 32)) * 2048)
+              : (uint64_t)(uintptr_t)(dst + ((int64_t)(b * Hq + hq) * S + k0w) * S);
+  };
+  const uint32_t dsoff = KT ? 2u * (uint32_t)(r * 32 + 8 * hh) : 2u * (uint32_t)(r * S + 8 * hh);
   // QM staging image of the wave's stage tile: [64 keys][32 queries] bf16, 64-B rows, 16-B chunks XOR-swizzled
   // by (key >> 1) & 3. Writes: lane (key r of block c, queries 16s + 8hh ..) -> chunk 2s + hh. Transposed reads:
   // lane group G = lane >> 4 reads keys 16i + 4(G >> 1) + {0-3} and +8 (slot order) for queries 16(G & 1) + (lane & 15)
@@ -354,7 +364,9 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     // ---- dV^T += dO^T.P (16 MFMAs; each transposed fragment feeds both key blocks) beside dS = p * (dP - delta),
     // its packing and the transposed dS stores
     u32x4 sw0[2], sw1[2];
-    const uint64_t row0 = dsrow + 2ull * (uint64_t)qs0, row1 = row0 + 2ull * 32ull * (uint64_t)S;
+    // KT: the stage's tile (4 KB) and its second key block (keys 32..63: + 32 rows of 64 B)
+    const uint64_t row0 = KT ? dsrow + 4096ull * (uint64_t)qt : dsrow + 2ull * (uint64_t)qs0;
+    const uint64_t row1 = KT ? row0 + 2048ull : row0 + 2ull * 32ull * (uint64_t)S;
     auto st = [](const u32x4& w, uint64_t row, int s, uint32_t off) {
       // lane r holds key r, queries 16s + {0-3, 8-11} (+4 for hh = 1); one permlane32_swap per dword pairs the
       // halves into queries 16s + 8hh .. +7: 16 B per lane
@@ -603,15 +615,24 @@ static int dkdv64_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, cons
     if (Hq == Hkv) KOP_LAUNCH(true, true, 1, false);
     else KOP_LAUNCH(false, true, 1, false);
   }
-  if (!rev && Hq != Hkv) {  // forward stage order (A/B)
+  if (!rev && Hq != Hkv && qm) {  // forward stage order (A/B)
     if (blk_layout) KOP_LAUNCH_FWD(false, true, 0, true);
     else KOP_LAUNCH_FWD(false, true, 0, false);
   }
   if (Hq == Hkv) {
+    if (blk_layout && !qm) KOP_LAUNCH(true, false, 0, true);  // KT tiles
     if (blk_layout) KOP_LAUNCH(true, true, 0, true);
     else KOP_LAUNCH(true, true, 0, false);
   }
   const int hpw = pick_hpw(B, S, Hq, Hkv);
+  if (blk_layout && !qm) {  // KT tiles: dS stored straight from the accumulators
+    switch (hpw) {
+      case 2: if (grp == 2) KOP_LAUNCH_R(true, false, 0, true, true, 2); else KOP_LAUNCH_R(false, false, 0, true, true, 2);
+      case 4: if (grp == 4) KOP_LAUNCH_R(true, false, 0, true, true, 4); else KOP_LAUNCH_R(false, false, 0, true, true, 4);
+      case 8: if (grp == 8) KOP_LAUNCH_R(true, false, 0, true, true, 8); else KOP_LAUNCH_R(false, false, 0, true, true, 8);
+      default: KOP_LAUNCH(false, false, 0, true);
+    }
+  }
   if (blk_layout) {
     switch (hpw) {
       case 2: if (grp == 2) KOP_LAUNCH_R(true, true, 0, true, true, 2); else KOP_LAUNCH_R(false, true, 0, true, true, 2);

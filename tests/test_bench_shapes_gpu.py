@@ -62,8 +62,9 @@ def _attention_reference(qkv, do, B, S, Hq, Hkv, D):
 
 
 @pytest.mark.parametrize("B,S,Hq,Hkv,D,cfg", [(1, 8192, 32, 8, 128, 64), (1, 8192, 32, 8, 128, 66),
-                                               (1, 8192, 32, 8, 128, 42), (8, 1024, 12, 12, 64, 42)],
-                         ids=["llama3_8b", "llama3_8b-dkdv66", "llama3_8b-dkdv42", "gpt2_small"])
+                                               (1, 8192, 32, 8, 128, 67), (1, 8192, 32, 8, 128, 42),
+                                               (8, 1024, 12, 12, 64, 42)],
+                         ids=["llama3_8b", "llama3_8b-dkdv66", "llama3_8b-dkdv67_kmaj", "llama3_8b-dkdv42", "gpt2_small"])
 def test_flash_attention_at_bench_shape(B, S, Hq, Hkv, D, cfg):
     from kubeoperator_amd.ops import load
     from kubeoperator_amd.ops.functional import rope_attention

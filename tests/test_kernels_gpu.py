@@ -359,9 +359,10 @@ def test_weight_grad_tn_layout_matches_nt(layout, monkeypatch):
         assert rel_err(out, 2 * ref) < 1e-2
 
 
-@pytest.mark.parametrize("variant,cfg", [(10, 64), (10, 66), (10, 640), (10, 42), (9, 64), (9, 42), (8, 42)],
-                         ids=["ds_blk-dkdv64", "ds-dkdv66", "ds_blk-dkdv64_d64", "ds-dkdv42", "recompute9-dkdv64",
-                              "recompute9", "recompute8"])
+@pytest.mark.parametrize("variant,cfg", [(10, 64), (10, 66), (10, 67), (10, 640), (10, 670), (10, 42), (9, 64), (9, 42),
+                                         (8, 42)],
+                         ids=["ds_blk-dkdv64", "ds-dkdv66", "ds_kmaj-dkdv67", "ds_blk-dkdv64_d64", "ds_kmaj-dkdv67_d64",
+                              "ds-dkdv42", "recompute9-dkdv64", "recompute9", "recompute8"])
 @pytest.mark.parametrize("D,Hq,Hkv,S", [(128, 8, 2, 512), (64, 4, 4, 256), (128, 4, 1, 768), (128, 8, 1, 256),
                                         (64, 8, 4, 512), (128, 4, 4, 512), (128, 6, 2, 512), (128, 2, 1, 256)])
 @pytest.mark.parametrize("causal", [True, False])
@@ -395,7 +396,8 @@ def test_flash_attention_bwd_dq_variants(variant, cfg, D, Hq, Hkv, S, causal):
 
 @pytest.mark.parametrize("hpw", [2, 4, 8])
 @pytest.mark.parametrize("D,cfg,B,S,Hq,Hkv", [(128, 64, 1, 768, 8, 2), (128, 64, 2, 512, 8, 1), (128, 64, 1, 1024, 16, 2),
-                                              (64, 640, 1, 512, 8, 1)])
+                                              (64, 640, 1, 512, 8, 1), (128, 67, 1, 768, 8, 2), (128, 67, 2, 512, 8, 1),
+                                              (64, 670, 1, 512, 8, 1)])
 @pytest.mark.parametrize("causal", [True, False])
 def test_dkdv_head_sweep_matches_one_head_per_workgroup(hpw, D, cfg, B, S, Hq, Hkv, causal):
     """The one-wave dK/dV kernel sweeping HPW query heads of a GQA group per workgroup (csrc/flash_bwd_w1.hip: the

@@ -680,10 +680,11 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq8_kernel(
 // a causal mask) makes this kernel HBM-bound, ~3x cheaper than recomputing.
 // BLK: dS in the wave-block layout of fa_bwd_dkdv64_kernel ([B, Hq, S/32, S/64, 32 queries, 64 slots]); the
 // tile's dS rows of one head and 32-query stage are then one contiguous 4-KB block.
-// KMAJ: dS in the key-major tiles of fa_bwd_dkdv64_kernel<QM = false, BLK> ([B, Hq, S/64, S/32, 64 keys, 32 queries]):
-// each wave's 32 query rows of a 64-key tile are one such 4-KB tile, copied lane-linear into LDS and read with
-// ds_read_b64_tr_b16 (rows = keys 64 B apart: one 32-lane half reads 4 consecutive rows, 256 B, conflict-free); the
-// two transposed reads of a k-step take keys R0 + 4hh + 0..3 and R0 + 8 + 4hh + 0..3, the k order of the K^T operand.
+// KMAJ: dS in the tiles of fa_bwd_dkdv64_kernel<QM = false, BLK> ([B, Hq, S/64, S/32] x 4 KB: block 2c + s holds keys
+// 32c + r, queries 16s + 8hh + j at chunk 32hh + (r ^ 4hh ^ 8s), element j): each wave's 32 query rows of a 64-key tile
+// are one such tile, copied lane-linear into LDS and read with ds_read_b64_tr_b16 -- lane 4q + p of a 16-lane group
+// names key row q (4 consecutive elements = 4 queries); the XOR spreads one 32-lane half's 32 reads over all 64 banks.
+// The two transposed reads of a k-step take keys R0 + 4hh + 0..3 and R0 + 8 + 4hh + 0..3, the K^T operand's k order.
 template <int D, int HP, bool BLK = false, bool NTL = false, bool KMAJ = false>
 __global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __restrict__ ds, const bf16_t* __restrict__ k,
                                                               bf16_t* __restrict__ dq, int B, int S, int Hq, int Hkv,
@@ -747,9 +748,12 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __re
   // dS row reads of image row 32*wid + r at chunk 2*ks4 + hh in the sub-tiled [256][128 B] image
   const int ds_lane0 = 4096 * wid + 1024 * (r >> 3) + 64 * (r & 7) + 16 * (hh ^ ((r >> 2) & 3));
   const int ds_lane1 = 4096 * wid + 1024 * (r >> 3) + 64 * (r & 7) + 16 * ((2 + hh) ^ ((r >> 2) & 3));
-  // KMAJ transposed reads of the wave's [64 keys][32 queries] tile: lane 4q + p of its 16-lane group gives row (key)
-  // R0 + 4hh + q, queries 16 tg1 + 4p .. +3
-  const int dk_lane = 4096 * wid + 64 * (4 * hh + tq) + 32 * tg1 + 8 * tp;
+  // KMAJ transposed reads: lane 4q + p of its 16-lane group names key R0 + 4hh + q (+8 for the second read), queries
+  // 16 tg1 + 4p .. +3, i.e. query half s = tg1, store half p >> 1, element 4 (p & 1); R0 = 16 ks4 adds 2048 (ks4 >> 1)
+  // + 256 (ks4 & 1) bytes
+  const int kr1 = 4 * hh + tq, kr2 = kr1 + 8, ksh = tp >> 1;
+  const int dk_lane = 4096 * wid + 1024 * tg1 + 16 * (32 * ksh + (kr1 ^ (4 * ksh) ^ (8 * tg1))) + 8 * (tp & 1);
+  const int dk_lane2 = 4096 * wid + 1024 * tg1 + 16 * (32 * ksh + (kr2 ^ (4 * ksh) ^ (8 * tg1))) + 8 * (tp & 1);
   f32x16 acc[DT];
 #pragma unroll
   for (int i = 0; i < DT; ++i) acc[i] = f32x16{0};
@@ -767,12 +771,14 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __re
       const uint32_t kb0 = lds_addr(sl) + kb_lane0, kb1 = lds_addr(sl) + kb_lane1;
       const uint32_t db0 = lds_addr(sl + KT) + ds_lane0, db1 = lds_addr(sl + KT) + ds_lane1;
       bf16x8 f[4];
-      const uint32_t dk0 = lds_addr(sl + KT) + dk_lane;
+      const uint32_t dk0 = lds_addr(sl + KT) + dk_lane, dk1 = lds_addr(sl + KT) + dk_lane2;
       (void)dk0;
+      (void)dk1;
       static_for<4>([&](auto ks4c) {
         constexpr int ks4 = decltype(ks4c)::value;
         if constexpr (KMAJ)
-          f[ks4] = cat44(lds_tr_read_off<1024 * ks4>(dk0), lds_tr_read_off<1024 * ks4 + 512>(dk0));
+          f[ks4] = cat44(lds_tr_read_off<2048 * (ks4 >> 1) + 256 * (ks4 & 1)>(dk0),
+                         lds_tr_read_off<2048 * (ks4 >> 1) + 256 * (ks4 & 1)>(dk1));
         else
           f[ks4] = lds_read8_off<512 * (ks4 >> 1)>((ks4 & 1) ? db1 : db0);
       });

@@ -91,12 +91,13 @@ __device__ __forceinline__ void vm_wait_le(int n) {
 // stored straight from the accumulators, measured slower and is no longer launched: profiles/r3_experiments.md.)
 // BLK (with QM): wave-block dS layout [B, Hq, S/32, S/64, 32 queries, 64 slots]: a wave's stage tile is one contiguous
 // 4 KB block (its workgroup's stage: 16 KB), instead of 32 rows of 128 B spread 2*S bytes apart.
-// KT (QM = false with BLK): key-major tiles [B, Hq, S/64, S/32, 64 keys, 32 queries], natural key and query order: a
-// wave's stage tile is again one contiguous 4 KB block, but stored straight from the accumulators (one
-// v_permlane32_swap per dword pairs the lane halves into 8-query runs; 4 dwordx4 stores whose partial lines all come
-// from this wave in this stage and merge in L2) -- no LDS staging. The stage is LDS-bandwidth bound and the staging
-// was 8 of the ~48 KB a wave moves through LDS per stage (profiles/r4_experiments.md); fa_bwd_dq_ds_kernel<KT> reads
-// the tiles back with ds_read_b64_tr_b16.
+// KT (QM = false with BLK): dS tiles of [B, Hq, S/64, S/32] stored straight from the accumulators -- no LDS staging
+// (its ds_write_b128s are the slow LDS path). One v_permlane32_swap per dword leaves lane (r, hh) holding key r
+// (+32 c for key block c), queries 16 s + 8 hh .. +7 of query half s as 16 B; a wave's stage tile is 4 KB = four 1-KB
+// blocks (c, s), and lane (r, hh) puts its 16 B at chunk 32 hh + (r ^ 4 hh ^ 8 s) of block 2 c + s. Every store
+// instruction then writes one whole 1-KB block, each 16-lane quarter two whole 128-B lines (a plain [64 keys][32
+// queries] tile had each quarter write 16 B into 16 rows: 4 stores per stage then cost 14 % of the kernel). The XOR
+// keeps the dQ kernel's ds_read_b64_tr_b16 reads of the tile conflict-free (fa_bwd_dq_ds_kernel<KMAJ>).
 // REV: sweep the query stages from the last one down to the workgroup's diagonal. Every workgroup of a head then
 // reads the same Q / dO stage at the same time (forward order starts workgroup kb 8*kb stages later, so a stage is
 // re-read ~16 us apart -- long enough for the dS write stream to evict it from the XCD's 4 MB L2).
@@ -208,7 +209,9 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     return KT ? (uint64_t)(uintptr_t)(dst + (((int64_t)(b * Hq + hq) * (S / 64) + k0w / 64) * (S / 32)) * 2048)
               : (uint64_t)(uintptr_t)(dst + ((int64_t)(b * Hq + hq) * S + k0w) * S);
   };
-  const uint32_t dsoff = KT ? 2u * (uint32_t)(r * 32 + 8 * hh) : 2u * (uint32_t)(r * S + 8 * hh);
+  const uint32_t dsoff = 2u * (uint32_t)(r * S + 8 * hh);
+  // KT: byte offset of lane (r, hh)'s 16-B chunk in block (c, s): the s = 0 / s = 1 forms (c adds 2048 B)
+  const uint32_t kto0 = 16u * (uint32_t)(32 * hh + (r ^ (4 * hh))), kto1 = 1024u + 16u * (uint32_t)(32 * hh + (r ^ (4 * hh) ^ 8));
   // QM staging image of the wave's stage tile: [64 keys][32 queries] bf16, 64-B rows, 16-B chunks XOR-swizzled
   // by (key >> 1) & 3. Writes: lane (key r of block c, queries 16s + 8hh ..) -> chunk 2s + hh. Transposed reads:
   // lane group G = lane >> 4 reads keys 16i + 4(G >> 1) + {0-3} and +8 (slot order) for queries 16(G & 1) + (lane & 15)
@@ -367,7 +370,7 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     // KT: the stage's tile (4 KB) and its second key block (keys 32..63: + 32 rows of 64 B)
     const uint64_t row0 = KT ? dsrow + 4096ull * (uint64_t)qt : dsrow + 2ull * (uint64_t)qs0;
     const uint64_t row1 = KT ? row0 + 2048ull : row0 + 2ull * 32ull * (uint64_t)S;
-    auto st = [](const u32x4& w, uint64_t row, int s, uint32_t off) {
+    auto st = [](const u32x4& w, uint64_t row, int s, uint32_t off) {  // KT: s is folded into off (s = 0 passed)
       // lane r holds key r, queries 16s + {0-3, 8-11} (+4 for hh = 1); one permlane32_swap per dword pairs the
       // halves into queries 16s + 8hh .. +7: 16 B per lane
       const auto a = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
@@ -410,8 +413,12 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
             stage_w<hs>(sw0[hs], hs ? stw1 : stw0, std::integral_constant<int, 0>{});
             stage_w<hs>(sw1[hs], hs ? stw1 : stw0, std::integral_constant<int, 2048>{});
           } else {
-            st(sw0[hs], row0, hs, dsoff);
-            st(sw1[hs], row1, hs, dsoff);
+            if constexpr (KT) {
+              // stored in the dK phase below, one per step behind its MFMAs
+            } else {
+              st(sw0[hs], row0, hs, dsoff);
+              st(sw1[hs], row1, hs, dsoff);
+            }
           }
         }
       });
@@ -454,6 +461,14 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
         mfma32_agpr(dk1[dt], cat44(t[2 * s], t[2 * s + 1]), sb1[s]);
       }
       if constexpr (dt + 1 < DT) trr(qa0, qa1, std::integral_constant<int, dt + 1>{}, ((DT + dt) & 1) ? ta : tb);
+      if constexpr (KT && !(DIAG & 1)) {
+        // the 4 dS stores spread over the dK steps (each blocks its wave while the CU's store path takes its 1 KB;
+        // bunched 2 + 2 in the dV phase they were exposed): store u = (key block u & 1, query half u >> 1)
+        static_for<4 / DT>([&](auto uc) {
+          constexpr int u = dt * (4 / DT) + decltype(uc)::value, c = u & 1, hs = u >> 1;
+          st(c ? sw1[hs] : sw0[hs], c ? row1 : row0, 0, hs ? kto1 : kto0);
+        });
+      }
       if constexpr (QM && !(DIAG & 1))
         static_for<SPI>([&](auto uc) {
           constexpr int u = decltype(uc)::value, I = dt * SPI + u;
@@ -626,6 +641,7 @@ static int dkdv64_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, cons
   }
   const int hpw = pick_hpw(B, S, Hq, Hkv);
   if (blk_layout && !qm) {  // KT tiles: dS stored straight from the accumulators
+    if (diag == 1 && hpw == 2 && grp != 2) KOP_LAUNCH_R(false, false, 1, true, true, 2);  // ablation: no dS stores
     switch (hpw) {
       case 2: if (grp == 2) KOP_LAUNCH_R(true, false, 0, true, true, 2); else KOP_LAUNCH_R(false, false, 0, true, true, 2);
       case 4: if (grp == 4) KOP_LAUNCH_R(true, false, 0, true, true, 4); else KOP_LAUNCH_R(false, false, 0, true, true, 4);

@@ -370,14 +370,23 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     // KT: the stage's tile (4 KB) and its second key block (keys 32..63: + 32 rows of 64 B)
     const uint64_t row0 = KT ? dsrow + 4096ull * (uint64_t)qt : dsrow + 2ull * (uint64_t)qs0;
     const uint64_t row1 = KT ? row0 + 2048ull : row0 + 2ull * 32ull * (uint64_t)S;
-    auto st = [](const u32x4& w, uint64_t row, int s, uint32_t off) {  // KT: s is folded into off (s = 0 passed)
+    // KT: s is folded into off (s = 0 passed). The KT stores go out non-temporally (nt): dS is read back once, by the
+    // dQ kernel, and left to the default policy its 2.15 GB stream pushed the Q / dO / K lines the stages re-read out of
+    // each XCD's L2 -- causal backward 1.659 / 1.668 ms vs 1.718 / 1.720 plain, sc1 1.697 / 1.690 (same box; on the
+    // LDS-staged layout both policies had measured slower: r4_experiments.md). DIAG 64 / 128: sc1 / plain (A/B)
+    auto st = [](const u32x4& w, uint64_t row, int s, uint32_t off) {
       // lane r holds key r, queries 16s + {0-3, 8-11} (+4 for hh = 1); one permlane32_swap per dword pairs the
       // halves into queries 16s + 8hh .. +7: 16 B per lane
       const auto a = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
       const auto c = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
       const u32x4 o = {a[0], c[0], a[1], c[1]};
       const uint64_t rs = row + 32ull * (uint64_t)s;
-      asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" ::"v"(off), "v"(o), "s"(rs) : "memory");
+      if constexpr (KT && (DIAG & 64))
+        asm volatile("global_store_dwordx4 %0, %1, %2 sc1\n\ts_nop 1" ::"v"(off), "v"(o), "s"(rs) : "memory");
+      else if constexpr (KT && !(DIAG & 128))
+        asm volatile("global_store_dwordx4 %0, %1, %2 nt\n\ts_nop 1" ::"v"(off), "v"(o), "s"(rs) : "memory");
+      else
+        asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" ::"v"(off), "v"(o), "s"(rs) : "memory");
     };
     static_for<DT>([&](auto dtc) {
       constexpr int dt = decltype(dtc)::value;
@@ -642,6 +651,8 @@ static int dkdv64_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, cons
   const int hpw = pick_hpw(B, S, Hq, Hkv);
   if (blk_layout && !qm) {  // KT tiles: dS stored straight from the accumulators
     if (diag == 1 && hpw == 2 && grp != 2) KOP_LAUNCH_R(false, false, 1, true, true, 2);  // ablation: no dS stores
+    if (diag == 64 && hpw == 2 && grp != 2) KOP_LAUNCH_R(false, false, 64, true, true, 2);  // sc1 dS stores
+    if (diag == 128 && hpw == 2 && grp != 2) KOP_LAUNCH_R(false, false, 128, true, true, 2);  // plain dS stores
     switch (hpw) {
       case 2: if (grp == 2) KOP_LAUNCH_R(true, false, 0, true, true, 2); else KOP_LAUNCH_R(false, false, 0, true, true, 2);
       case 4: if (grp == 4) KOP_LAUNCH_R(true, false, 0, true, true, 4); else KOP_LAUNCH_R(false, false, 0, true, true, 4);

@@ -680,8 +680,9 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq8_kernel(
 // a causal mask) makes this kernel HBM-bound, ~3x cheaper than recomputing.
 // BLK: dS in the wave-block layout of fa_bwd_dkdv64_kernel ([B, Hq, S/32, S/64, 32 queries, 64 slots]); the
 // tile's dS rows of one head and 32-query stage are then one contiguous 4-KB block.
-// KMAJ: dS in the tiles of fa_bwd_dkdv64_kernel<QM = false, BLK> ([B, Hq, S/64, S/32] x 4 KB: block 2c + s holds keys
-// 32c + r, queries 16s + 8hh + j at chunk 32hh + (r ^ 4hh ^ 8s), element j): each wave's 32 query rows of a 64-key tile
+// KMAJ: dS in the tiles of fa_bwd_dkdv64_kernel<QM = false, BLK> ([B, Hq, S/64, S/32] x 4 KB: block 2c + s holds, for
+// key 32c + r, queries 16s + 4hh + 0..3 and 16s + 8 + 4hh + 0..3 as the two 8-B halves of chunk 32hh + (r ^ 4hh ^ 8s)):
+// each wave's 32 query rows of a 64-key tile
 // are one such tile, copied lane-linear into LDS and read with ds_read_b64_tr_b16 -- lane 4q + p of a 16-lane group
 // names key row q (4 consecutive elements = 4 queries); the XOR spreads one 32-lane half's 32 reads over all 64 banks.
 // The two transposed reads of a k-step take keys R0 + 4hh + 0..3 and R0 + 8 + 4hh + 0..3, the K^T operand's k order.
@@ -749,11 +750,11 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __re
   const int ds_lane0 = 4096 * wid + 1024 * (r >> 3) + 64 * (r & 7) + 16 * (hh ^ ((r >> 2) & 3));
   const int ds_lane1 = 4096 * wid + 1024 * (r >> 3) + 64 * (r & 7) + 16 * ((2 + hh) ^ ((r >> 2) & 3));
   // KMAJ transposed reads: lane 4q + p of its 16-lane group names key R0 + 4hh + q (+8 for the second read), queries
-  // 16 tg1 + 4p .. +3, i.e. query half s = tg1, store half p >> 1, element 4 (p & 1); R0 = 16 ks4 adds 2048 (ks4 >> 1)
-  // + 256 (ks4 & 1) bytes
-  const int kr1 = 4 * hh + tq, kr2 = kr1 + 8, ksh = tp >> 1;
-  const int dk_lane = 4096 * wid + 1024 * tg1 + 16 * (32 * ksh + (kr1 ^ (4 * ksh) ^ (8 * tg1))) + 8 * (tp & 1);
-  const int dk_lane2 = 4096 * wid + 1024 * tg1 + 16 * (32 * ksh + (kr2 ^ (4 * ksh) ^ (8 * tg1))) + 8 * (tp & 1);
+  // 16 tg1 + 4p .. +3, i.e. query half s = tg1, storing lane half p & 1, 8-B half p >> 1 of its chunk; R0 = 16 ks4 adds
+  // 2048 (ks4 >> 1) + 256 (ks4 & 1) bytes
+  const int kr1 = 4 * hh + tq, kr2 = kr1 + 8, ksh = tp & 1;
+  const int dk_lane = 4096 * wid + 1024 * tg1 + 16 * (32 * ksh + (kr1 ^ (4 * ksh) ^ (8 * tg1))) + 8 * (tp >> 1);
+  const int dk_lane2 = 4096 * wid + 1024 * tg1 + 16 * (32 * ksh + (kr2 ^ (4 * ksh) ^ (8 * tg1))) + 8 * (tp >> 1);
   f32x16 acc[DT];
 #pragma unroll
   for (int i = 0; i < DT; ++i) acc[i] = f32x16{0};

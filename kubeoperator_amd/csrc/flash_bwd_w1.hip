@@ -92,9 +92,10 @@ __device__ __forceinline__ void vm_wait_le(int n) {
 // BLK (with QM): wave-block dS layout [B, Hq, S/32, S/64, 32 queries, 64 slots]: a wave's stage tile is one contiguous
 // 4 KB block (its workgroup's stage: 16 KB), instead of 32 rows of 128 B spread 2*S bytes apart.
 // KT (QM = false with BLK): dS tiles of [B, Hq, S/64, S/32] stored straight from the accumulators -- no LDS staging
-// (its ds_write_b128s are the slow LDS path). One v_permlane32_swap per dword leaves lane (r, hh) holding key r
-// (+32 c for key block c), queries 16 s + 8 hh .. +7 of query half s as 16 B; a wave's stage tile is 4 KB = four 1-KB
-// blocks (c, s), and lane (r, hh) puts its 16 B at chunk 32 hh + (r ^ 4 hh ^ 8 s) of block 2 c + s. Every store
+// (its ds_write_b128s are the slow LDS path) and no lane exchange: lane (r, hh)'s packed register quad s holds key r
+// (+32 c for key block c), queries 16 s + 4 hh + 0..3 and 16 s + 8 + 4 hh + 0..3 (two 8-B runs); a wave's stage tile is
+// 4 KB = four 1-KB blocks (c, s), and the lane stores the quad as-is at chunk 32 hh + (r ^ 4 hh ^ 8 s) of block 2 c + s
+// (a v_permlane32_swap pairing into 8-query runs first cost 8 cross-lane ops per stage). Every store
 // instruction then writes one whole 1-KB block, each 16-lane quarter two whole 128-B lines (a plain [64 keys][32
 // queries] tile had each quarter write 16 B into 16 rows: 4 stores per stage then cost 14 % of the kernel). The XOR
 // keeps the dQ kernel's ds_read_b64_tr_b16 reads of the tile conflict-free (fa_bwd_dq_ds_kernel<KMAJ>).
@@ -368,25 +369,29 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     // its packing and the transposed dS stores
     u32x4 sw0[2], sw1[2];
     // KT: the stage's tile (4 KB) and its second key block (keys 32..63: + 32 rows of 64 B)
-    const uint64_t row0 = KT ? dsrow + 4096ull * (uint64_t)qt : dsrow + 2ull * (uint64_t)qs0;
+    // DIAG 256 (timing ablation, wrong dQ): every stage's KT stores go to the wave's first tile (same 4 KB)
+    const uint64_t row0 = KT ? dsrow + ((DIAG & 256) ? 0ull : 4096ull * (uint64_t)qt) : dsrow + 2ull * (uint64_t)qs0;
     const uint64_t row1 = KT ? row0 + 2048ull : row0 + 2ull * 32ull * (uint64_t)S;
-    // KT: s is folded into off (s = 0 passed). The KT stores go out non-temporally (nt): dS is read back once, by the
-    // dQ kernel, and left to the default policy its 2.15 GB stream pushed the Q / dO / K lines the stages re-read out of
-    // each XCD's L2 -- causal backward 1.659 / 1.668 ms vs 1.718 / 1.720 plain, sc1 1.697 / 1.690 (same box; on the
-    // LDS-staged layout both policies had measured slower: r4_experiments.md). DIAG 64 / 128: sc1 / plain (A/B)
-    auto st = [](const u32x4& w, uint64_t row, int s, uint32_t off) {
+    auto st = [](const u32x4& w, uint64_t row, int s, uint32_t off) {  // the row-major transposed layout (QM = false)
       // lane r holds key r, queries 16s + {0-3, 8-11} (+4 for hh = 1); one permlane32_swap per dword pairs the
       // halves into queries 16s + 8hh .. +7: 16 B per lane
       const auto a = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
       const auto c = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
       const u32x4 o = {a[0], c[0], a[1], c[1]};
       const uint64_t rs = row + 32ull * (uint64_t)s;
-      if constexpr (KT && (DIAG & 64))
-        asm volatile("global_store_dwordx4 %0, %1, %2 sc1\n\ts_nop 1" ::"v"(off), "v"(o), "s"(rs) : "memory");
-      else if constexpr (KT && !(DIAG & 128))
-        asm volatile("global_store_dwordx4 %0, %1, %2 nt\n\ts_nop 1" ::"v"(off), "v"(o), "s"(rs) : "memory");
+      asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" ::"v"(off), "v"(o), "s"(rs) : "memory");
+    };
+    // KT: the packed quad as-is (see the layout note), non-temporally (nt): dS is read back once, by the dQ kernel, and
+    // left to the default policy its 2.15 GB stream pushed the Q / dO / K lines the stages re-read out of each XCD's L2
+    // -- causal backward 1.659 / 1.668 ms vs 1.718 / 1.720 plain, sc1 1.697 / 1.690 (same box; on the LDS-staged layout
+    // both policies had measured slower: r4_experiments.md). DIAG 64 / 128: sc1 / plain (A/B)
+    auto st_kt = [](const u32x4& w, uint64_t row, uint32_t off) {
+      if constexpr (DIAG & 64)
+        asm volatile("global_store_dwordx4 %0, %1, %2 sc1\n\ts_nop 1" ::"v"(off), "v"(w), "s"(row) : "memory");
+      else if constexpr (!(DIAG & 128))
+        asm volatile("global_store_dwordx4 %0, %1, %2 nt\n\ts_nop 1" ::"v"(off), "v"(w), "s"(row) : "memory");
       else
-        asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" ::"v"(off), "v"(o), "s"(rs) : "memory");
+        asm volatile("global_store_dwordx4 %0, %1, %2\n\ts_nop 1" ::"v"(off), "v"(w), "s"(row) : "memory");
     };
     static_for<DT>([&](auto dtc) {
       constexpr int dt = decltype(dtc)::value;
@@ -475,7 +480,7 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
         // bunched 2 + 2 in the dV phase they were exposed): store u = (key block u & 1, query half u >> 1)
         static_for<4 / DT>([&](auto uc) {
           constexpr int u = dt * (4 / DT) + decltype(uc)::value, c = u & 1, hs = u >> 1;
-          st(c ? sw1[hs] : sw0[hs], c ? row1 : row0, 0, hs ? kto1 : kto0);
+          st_kt(c ? sw1[hs] : sw0[hs], c ? row1 : row0, hs ? kto1 : kto0);
         });
       }
       if constexpr (QM && !(DIAG & 1))
@@ -653,6 +658,7 @@ static int dkdv64_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, cons
     if (diag == 1 && hpw == 2 && grp != 2) KOP_LAUNCH_R(false, false, 1, true, true, 2);  // ablation: no dS stores
     if (diag == 64 && hpw == 2 && grp != 2) KOP_LAUNCH_R(false, false, 64, true, true, 2);  // sc1 dS stores
     if (diag == 128 && hpw == 2 && grp != 2) KOP_LAUNCH_R(false, false, 128, true, true, 2);  // plain dS stores
+    if (diag == 256 && hpw == 2 && grp != 2) KOP_LAUNCH_R(false, false, 256, true, true, 2);  // stores to one tile
     switch (hpw) {
       case 2: if (grp == 2) KOP_LAUNCH_R(true, false, 0, true, true, 2); else KOP_LAUNCH_R(false, false, 0, true, true, 2);
       case 4: if (grp == 4) KOP_LAUNCH_R(true, false, 0, true, true, 4); else KOP_LAUNCH_R(false, false, 0, true, true, 4);

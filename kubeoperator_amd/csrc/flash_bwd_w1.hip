@@ -562,8 +562,10 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
   out(dk1, dv1, k0w + 32 + r);
 }
 
-// heads per workgroup: the largest power of two dividing the GQA group that still leaves >= 2 workgroups per CU
-// (the causal key blocks differ 32x in work; fewer, longer workgroups would end on a few heavy ones).
+// heads per workgroup: the largest power of two dividing the GQA group that still leaves >= 2 workgroups per CU under
+// a causal mask (the causal key blocks differ 32x in work; fewer, longer workgroups would end on a few heavy ones), >= 1
+// without one (equal work per workgroup: fewer partials win -- Llama-3-8B shape non-causal 2.862 / 2.861 ms with HPW 4
+// vs 2.899 / 2.940 with 2, causal 2.14 vs 1.65 ms: profiles/r4_dkdv_hpw_recheck.jsonl).
 // KOP_DKDV_HPW / flash_attn_set_dkdv_hpw override it (1 / 2 / 4 / 8; 0 automatic).
 static int g_hpw = -1;  // -1: read KOP_DKDV_HPW on first use; 0: automatic; 1 / 2 / 4 / 8: forced
 int flash_attn_set_dkdv_hpw(int h) {
@@ -575,7 +577,7 @@ int flash_attn_set_dkdv_hpw(int h) {
   if (h >= 0) g_hpw = h;
   return old;
 }
-static int pick_hpw(int B, int S, int Hq, int Hkv) {
+static int pick_hpw(int B, int S, int Hq, int Hkv, bool causal) {
   const int env = flash_attn_set_dkdv_hpw(-1);
   const int grp = Hq / Hkv;
   if (env > 0) return (grp % env == 0 && env <= 8) ? env : 1;
@@ -586,7 +588,8 @@ static int pick_hpw(int B, int S, int Hq, int Hkv) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
   }
   int h = 1;
-  while (h * 2 <= 8 && grp % (h * 2) == 0 && (int64_t)B * (Hq / (h * 2)) * (S / 256) >= 2 * (int64_t)cus) h *= 2;
+  const int64_t min_wg = (causal ? 2 : 1) * (int64_t)cus;
+  while (h * 2 <= 8 && grp % (h * 2) == 0 && (int64_t)B * (Hq / (h * 2)) * (S / 256) >= min_wg) h *= 2;
   return h;
 }
 
@@ -653,7 +656,7 @@ static int dkdv64_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, cons
     if (blk_layout) KOP_LAUNCH(true, true, 0, true);
     else KOP_LAUNCH(true, true, 0, false);
   }
-  const int hpw = pick_hpw(B, S, Hq, Hkv);
+  const int hpw = pick_hpw(B, S, Hq, Hkv, causal != 0);
   if (blk_layout && !qm) {  // KT tiles: dS stored straight from the accumulators
     if (diag == 1 && hpw == 2 && grp != 2) KOP_LAUNCH_R(false, false, 1, true, true, 2);  // ablation: no dS stores
     if (diag == 64 && hpw == 2 && grp != 2) KOP_LAUNCH_R(false, false, 64, true, true, 2);  // sc1 dS stores

@@ -1003,7 +1003,12 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
     const int cfg = dkdv_cfg();
     const int cflag = causal ? 1 : 0;
     const int grp = Hq / Hkv;  // heads per dQ workgroup: largest power of two dividing the GQA group, <= 8
-    const int hp = (grp % 8 == 0) ? 8 : (grp % 4 == 0) ? 4 : (grp % 2 == 0) ? 2 : 1;
+    static const int hp_env = [] {  // KOP_DQ_HP: force the dQ kernel's heads per workgroup (A/B)
+      const char* e = getenv("KOP_DQ_HP");
+      return e ? atoi(e) : 0;
+    }();
+    const int hp = (hp_env > 0 && grp % hp_env == 0 && hp_env <= 8) ? hp_env
+                   : (grp % 8 == 0) ? 8 : (grp % 4 == 0) ? 4 : (grp % 2 == 0) ? 2 : 1;
     // one wave per SIMD (flash_bwd_w1.hip): query-major dS staged through LDS into whole-line stores, in the
     // wave-block layout (cfg 64; 640 = the same at D = 64, opt-in) or plain rows (66); cfg 67 / 670: key-major tiles
     // stored straight from the accumulators (no LDS staging), read back transposed by the dQ kernel

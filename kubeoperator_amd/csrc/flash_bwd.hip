@@ -1012,9 +1012,11 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
     // one wave per SIMD (flash_bwd_w1.hip): query-major dS staged through LDS into whole-line stores, in the
     // wave-block layout (cfg 64; 640 = the same at D = 64, opt-in) or plain rows (66); cfg 67 / 670: key-major tiles
     // stored straight from the accumulators (no LDS staging), read back transposed by the dQ kernel
-    const bool kmaj = (D == 128 && cfg == 67) || (D == 64 && cfg == 670);
+    // (the default 67 takes the key-major path at D = 64 as well: GPT-2-small backward at its bench shape 0.372 /
+    // 0.373 ms vs 0.402 / 0.400 with the two-waves-per-SIMD kernel, step +1.1 %: profiles/r4_gpt2_kmaj_d64_ab.jsonl)
+    const bool kmaj = (D == 128 && cfg == 67) || (D == 64 && (cfg == 67 || cfg == 670));
     const bool one_wave = S % 256 == 0 && ((D == 128 && (cfg == 64 || cfg == 66 || cfg == 67)) ||
-                                           (D == 64 && (cfg == 640 || cfg == 670)));
+                                           (D == 64 && (cfg == 640 || cfg == 670 || cfg == 67)));
     const bool blk = one_wave && cfg != 66;
     bool done = false;
     int np = direct ? 0 : Hq / Hkv;  // fp32 partials per GQA group left for the finalize pass

@@ -11,8 +11,11 @@ recorded, so tests assert on the exact command stream; fault injection comes fro
 from __future__ import annotations
 
 import base64
+import fnmatch
 import json
 import os
+import re
+import shlex
 import time
 
 from .transport import CmdResult, FakeTransport
@@ -46,6 +49,29 @@ users:
 """
 
 
+def _apt_install_args(cmd: str) -> list[str] | None:
+    """Package arguments of the apt-get install in a command (the package module's apt branch), or None."""
+    m = re.search(r"apt-get install (.*?)(?:;|&&|\|\||$)", cmd)
+    if not m:
+        return None
+    try:
+        words = shlex.split(m.group(1))
+    except ValueError:
+        return None
+    return [w for w in words if not w.startswith("-")]
+
+
+def _upstream3(v: str) -> str:
+    """'1:6.14.14.30200000-2204' -> '6.14.14', '7.0.0.70000-17~22.04' -> '7.0.0'."""
+    return ".".join(v.split(":", 1)[-1].split("-", 1)[0].split(".")[:3])
+
+
+def _dkms_probe_sed(v: str) -> str:
+    """What upgrade-gpu's version probe pipeline prints for a dpkg version string (its sed, in Python)."""
+    v = re.sub(r"^[0-9]+:", "", v)
+    return re.sub(r"^([0-9]+(\.[0-9]+)*).*", r"\1", v)
+
+
 class SimFarm(FakeTransport):
     def __init__(self, gpu_hosts: set | None = None, gpus_per_host: int = 8, latency_s: float = 0.0,
                  state_path: str | None = None):
@@ -64,7 +90,21 @@ class SimFarm(FakeTransport):
         # holders (a non-zero count makes the upgrade reboot instead of reloading) and the boot counter
         self.gpu_stack: dict[str, dict] = {}
         self.amdgpu_holders = 0
+        # Debian package state per host: installed version strings and apt-mark holds
+        self.apt_installed: dict[str, dict] = {}
+        self.apt_held: dict[str, set] = {}
         self._install_rules()
+
+    # The offline repository's versions of the pinned packages, ascending, as the vendors publish them: AMD's
+    # amdgpu-dkms carries epoch 1, rocm-core and the pkgs.k8s.io packages none (tests/test_apt_resolve.py builds
+    # real .debs with these strings and resolves the roles' pins with apt-get).
+    APT_CATALOG = {
+        "amdgpu-dkms": ["1:6.14.14.30200000-2204", "1:6.16.6.30300000-2204"],
+        "rocm-core": ["7.0.0.70000-17~22.04", "7.1.0.70100-20~22.04"],
+        "kubeadm": ["1.30.6-1.1", "1.31.2-1.1"],
+        "kubelet": ["1.30.6-1.1", "1.31.2-1.1"],
+        "kubectl": ["1.30.6-1.1", "1.31.2-1.1"],
+    }
 
     BASE_FILES = {
         "/etc/ssh/sshd_config": b"#UseDNS yes\nPermitRootLogin yes\n",
@@ -176,23 +216,51 @@ class SimFarm(FakeTransport):
             with self._lock:
                 return self.gpu_stack.setdefault(host, {"dkms": None, "rocm": None, "boot": 0})
 
-        def pkg_install(host, cmd, fs):  # record pinned GPU packages, then fall through to success
-            import re as _re
-
-            st = stack(host)
-            m = _re.search(r"amdgpu-dkms[=-]([0-9][0-9.]*[0-9])", cmd)
-            if m:
-                st["dkms"] = m.group(1)
-            m = _re.search(r"rocm-core[=-]([0-9][0-9.]*[0-9])", cmd)
-            if m:
-                st["rocm"] = m.group(1) + (".0" if m.group(1).count(".") == 1 else "")
+        def pkg_install(host, cmd, fs):
+            """apt-get install as apt resolves it: a "name=<pattern>" argument must match one of the repository's
+            version strings of that package WHOLE (epoch included) as a glob, and a held package may not change
+            version; otherwise apt's error and status 100. Installed versions are recorded per host."""
+            args = _apt_install_args(cmd)
+            if args is None:
+                return 0, "", ""
+            chosen = {}
+            for a in args:
+                name, _, pat = a.partition("=")
+                vers = self.APT_CATALOG.get(name)
+                if vers is None:  # a package the catalogue does not model: any name / version installs
+                    continue
+                hit = [v for v in vers if fnmatch.fnmatchcase(v, pat)] if pat else list(vers)
+                if not hit:
+                    return 100, "", f"E: Version '{pat}' for '{name}' was not found"
+                chosen[name] = hit[-1]  # catalogue order is ascending: apt's candidate is the highest match
+            with self._lock:
+                inst = self.apt_installed.setdefault(host, {})
+                held = self.apt_held.setdefault(host, set())
+                for name, v in chosen.items():
+                    if name in held and inst.get(name) not in (None, v):
+                        return 100, "", ("E: Held packages were changed and -y was used without "
+                                         "--allow-change-held-packages.")
+                inst.update(chosen)
+            if "amdgpu-dkms" in chosen:
+                stack(host)["dkms"] = _upstream3(chosen["amdgpu-dkms"])
+            if "rocm-core" in chosen:
+                stack(host)["rocm"] = _upstream3(chosen["rocm-core"])
             return 0, "", ""
 
-        def dkms_version(host, cmd, fs):  # the probe pipes dpkg-query's "1:6.14.14.30200000-2204" through sed
-            v = stack(host)["dkms"]
+        def apt_mark(host, cmd, fs):
+            words = cmd.split()
+            op, names = words[1], words[2:]
+            with self._lock:
+                held = self.apt_held.setdefault(host, set())
+                for n in names:
+                    (held.add if op == "hold" else held.discard)(n)
+            return 0, "".join(f"{n} set on hold.\n" if op == "hold" else f"Canceled hold on {n}.\n" for n in names), ""
+
+        def dkms_version(host, cmd, fs):  # dpkg-query's full version string; the probe strips it with sed
+            v = self.apt_installed.get(host, {}).get("amdgpu-dkms")
             if "sed" in cmd:
-                return 0, v or "none", ""
-            return (0, f"1:{v}.30200000-2204", "") if v else (1, "", "no packages found matching amdgpu-dkms")
+                return 0, _dkms_probe_sed(v) if v else "none", ""
+            return (0, v, "") if v else (1, "", "no packages found matching amdgpu-dkms")
 
         def rocm_version(host, cmd, fs):
             v = stack(host)["rocm"]
@@ -280,10 +348,12 @@ class SimFarm(FakeTransport):
         R(r"^helm status \S+ -n \S+ -o json", stdout="deployed")
         R(r"kubectl -n \S+ logs -l app.kubernetes.io/instance=", fn=train_log)
         R(r"systemctl is-active", rc=3)
-        R(r"apt-get install .*(amdgpu-dkms|rocm-core)[=-]", fn=pkg_install)
+        R(r"apt-get install ", fn=pkg_install)
+        R(r"^apt-mark (un)?hold ", fn=apt_mark)
         R(r"dpkg-query -W -f='\$\{Version\}' amdgpu-dkms", fn=dkms_version)
         R(r"^d=\$\( \(dpkg-query", fn=lambda h, c, fs: (
-            (0, f"{stack(h)['dkms']} {stack(h)['rocm']}", "") if stack(h)["dkms"] else (1, "", "not installed")))
+            (0, f"{self.apt_installed[h]['amdgpu-dkms'].split(':', 1)[-1]} {stack(h)['rocm']}", "")
+            if stack(h)["dkms"] else (1, "", "not installed")))
         R(r"cat /opt/rocm/\.info/version", fn=rocm_version)
         R(r"awk '\$1 == \"amdgpu\" \{print \$3\}' /proc/modules", fn=lambda h, c, fs: (0, str(self.amdgpu_holders), ""))
         R(r"nohup sh -c 'sleep 2; systemctl reboot'", fn=reboot)

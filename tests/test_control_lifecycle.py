@@ -126,7 +126,9 @@ def test_upgrade_moves_the_gpu_pool_to_the_package_versions(control):
         _first(log, "m1", r"kubectl drain w1"),
         _first(log, "m1", r"kubectl label node w1 kubeoperator\.io/gpu-$"),
         _first(log, "m1", r"amdgpu-dp-ds --field-selector spec\.nodeName=w1"),
-        _first(log, "w1", r"amdgpu-dkms=6\.16\.6"),
+        _first(log, "w1", r"^apt-mark unhold amdgpu-dkms rocm-core$"),
+        _first(log, "w1", r"'amdgpu-dkms=1:6\.16\.6\*' 'rocm-core=7\.1\*'"),  # apt pins carry the epoch
+        _first(log, "w1", r"^apt-mark hold amdgpu-dkms rocm-core$"),
         _first(log, "w1", r"modprobe -r amdgpu && modprobe amdgpu"),
         _first(log, "w1", r"kfd/topology/nodes/\*/gpu_id"),
         _first(log, "w1", r"rocminfo \| awk"),
@@ -137,6 +139,12 @@ def test_upgrade_moves_the_gpu_pool_to_the_package_versions(control):
     ]
     assert order == sorted(order), order
     assert not any(re.search(r"systemctl reboot", c) for _, c in log)  # no holders: reload, not reboot
+    assert farm.apt_installed["w1"]["amdgpu-dkms"] == "1:6.16.6.30300000-2204"
+    assert {"amdgpu-dkms", "rocm-core", "kubeadm", "kubelet", "kubectl"} <= farm.apt_held["w1"]
+    # kubeadm upgrade semantics: each Kubernetes package is released, moved and held again
+    for pkg in ("kubeadm", "kubelet"):
+        assert (_first(log, "w1", rf"^apt-mark unhold {pkg}\b") < _first(log, "w1", rf"'{pkg}=1\.31\.2\*'")
+                < _first(log, "w1", rf"^apt-mark hold {pkg}\b"))
     # masters: no GPU-stack commands at all
     assert not [c for h, c in log if h == "m1" and re.search(r"amdgpu-dkms|rocm-core|modprobe .*amdgpu", c)]
     # the node's apt sources now name the new ROCm and driver repositories
@@ -160,6 +168,21 @@ def test_gpu_upgrade_reboots_when_the_module_is_held(control):
     assert farm.gpu_stack["w1"]["boot"] == 1
     assert not any("modprobe -r amdgpu" in c for _, c in log)
     assert _first(log, "w1", r"systemctl reboot") < _first(log, "w1", r"kfd/topology/nodes/\*/gpu_id") \
+        < _first(log, "m1", r"kubectl uncordon w1")
+
+
+def test_gpu_upgrade_reboots_when_the_reload_fails(control):
+    """a holder that appears between the refcount read and the unload makes ``modprobe -r`` fail; the
+    node reboots instead of staying cordoned without GPUs."""
+    _cluster()
+    farm = control.farm
+    assert deploy.create("demo", "install", run="inline")["state"] == "SUCCESS"
+    farm.add_rule(r"^modprobe -r amdgpu && modprobe amdgpu$", rc=1, stderr="modprobe: FATAL: Module amdgpu is in use.")
+    e, log = _upgrade_slice(farm, lambda: deploy.create("demo", "upgrade", {"package": "mi355x-k8s-next"},
+                                                        run="inline"))
+    assert e["state"] == "SUCCESS", e["result_summary"].get("dark")
+    assert farm.gpu_stack["w1"]["boot"] == 1
+    assert _first(log, "w1", r"modprobe -r amdgpu") < _first(log, "w1", r"systemctl reboot") \
         < _first(log, "m1", r"kubectl uncordon w1")
 
 

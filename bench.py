@@ -23,7 +23,11 @@ over ranks): the compute stream's stall between backward's last kernel and the c
 collective, plus its stalls on ZeRO-1 all-gather gates in the next forward -- CUDA-event timed on the GPU.
 ``runtime`` records torch / HIP / RCCL versions and every ``NCCL_*`` / ``RCCL_*`` / ``HSA_*`` / ``TORCH_NCCL_*`` /
 ``HIP_*`` variable in effect; ``cpu_affinity_rank0`` the CPUs rank 0 was pinned to (N > 1: each rank is bound to
-its GPU's NUMA-local CPUs, ``parallel/dist.py`` ``bind_rank_cpus``).
+its GPU's NUMA-local CPUs and sizes its thread pool to them, ``parallel/dist.py`` ``bind_rank_cpus``, with the reason
+of any fallback). ``ranks`` (N > 1): one record per rank -- its pinning, its exposed waits (``finish_wait_ms``: the
+compute stream's stall for the last gradient collective; ``gate_wait_ms``: its stalls on ZeRO-1 all-gather gates) and
+its bucket timeline (``parallel/ddp.py`` ``timeline_summary``: when the buckets' gradients were ready and their
+collectives done, relative to backward's last kernel).
 """
 from __future__ import annotations
 
@@ -53,7 +57,9 @@ def _self_launch(n: int) -> int:
 
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL peer buffers)
-    env.setdefault("OMP_NUM_THREADS", "8")
+    # an even share of the CPUs this job may use per rank (each rank re-sizes its pool to the CPUs it is pinned to,
+    # parallel/dist.py bind_rank_cpus): a fixed count per rank oversubscribes a small CPU share N-fold
+    env["OMP_NUM_THREADS"] = str(max(1, len(os.sched_getaffinity(0)) // n))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
     print(f"[bench] --gpus {n} without torchrun: launching {n} ranks ({' '.join(cmd[1:6])} ...)", file=sys.stderr,
@@ -116,7 +122,7 @@ def main() -> int:
     import torch
 
     from kubeoperator_amd.parallel.dist import (all_reduce_max, barrier, bind_rank_cpus, collectives_on,
-                                                init_distributed, runtime_env, shutdown)
+                                                gather_objects, init_distributed, runtime_env, shutdown)
     from kubeoperator_amd.models import get_config
     from kubeoperator_amd.train import SyntheticTokens, TrainConfig, Trainer
 
@@ -160,6 +166,7 @@ def main() -> int:
     timing = cuda and collectives_on(info)
     if timing:  # exposed-communication events (a handful per step, no host synchronisation)
         trainer.dp.finish_waits, trainer.store.gate_waits = [], []
+        trainer.dp.timeline = []
     comm0, gather0 = trainer.dp.comm_bytes, trainer.dp.gather_bytes
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -170,12 +177,22 @@ def main() -> int:
     elapsed = time.perf_counter() - t0
     elapsed = all_reduce_max(elapsed, info)
     exposed_ms = None
+    ranks = None
     if timing:
         trainer.store.await_all()  # the next step's gates: their waits belong to the timed steps' collectives
         sync()
-        waits = trainer.dp.finish_waits + trainer.store.gate_waits
-        exposed_ms = all_reduce_max(sum(a.elapsed_time(b) for a, b in waits) / args.steps, info)
-        trainer.dp.finish_waits = trainer.store.gate_waits = None
+        fin = sum(a.elapsed_time(b) for a, b in trainer.dp.finish_waits) / args.steps
+        gate = sum(a.elapsed_time(b) for a, b in trainer.store.gate_waits) / args.steps
+        exposed_ms = all_reduce_max(fin + gate, info)
+        # per rank: what it was pinned to, its bucket timeline and its two exposed-wait components (all ranks' records
+        # land in rank 0's JSON line, so a slow rank or a late bucket is attributable)
+        from kubeoperator_amd.parallel.ddp import timeline_summary
+
+        rec = {"rank": info.rank, "affinity": affinity, "finish_wait_ms": round(fin, 3), "gate_wait_ms": round(gate, 3),
+               "gate_waits_per_step": len(trainer.store.gate_waits) // max(1, args.steps),
+               "buckets": timeline_summary(trainer.dp.timeline)}
+        ranks = gather_objects(rec, info)
+        trainer.dp.finish_waits = trainer.store.gate_waits = trainer.dp.timeline = None
     comm_step = (trainer.dp.comm_bytes - comm0) // max(1, args.steps)
     gather_step = (trainer.dp.gather_bytes - gather0) // max(1, args.steps)
     gemm_tuning.finish(tuning, info.rank)
@@ -233,6 +250,7 @@ def main() -> int:
             "param_gather_bytes_per_step": int(gather_step),
             "exposed_comm_ms": round(exposed_ms, 3) if exposed_ms is not None else None,
             "cpu_affinity_rank0": affinity,
+            "ranks": ranks,
             "runtime": runtime_env(),
         }
         print(json.dumps(out), flush=True)

@@ -55,6 +55,11 @@ class DataParallel:
         self.comm_bytes = 0  # gradient bytes handed to collectives (per rank, cumulative)
         self.gather_bytes = 0  # ZeRO-1 all-gather output bytes (per rank, cumulative)
         self.finish_waits: list | None = None  # (event, event) around finish_grads (exposed comm timing)
+        # bench: per optimizer step, every bucket's (index, grads-ready event, collective-done event) and backward's
+        # end, CUDA-event timed without host synchronisation (``timeline_summary`` turns them into a per-rank record)
+        self.timeline: list | None = None
+        self._tl_cur: list = []
+        self._tl_stream = None
         store.on_ready = self._on_ready
         self.overlapped = False  # set once the optimizer publishes ZeRO-1 gathers itself
         # one-rank RCCL self-test (parallel.dist.rccl_selftest): world-1 buckets still go through the collectives
@@ -77,11 +82,25 @@ class DataParallel:
             return
         g = self.store.grads[b.start:b.end]
         self.comm_bytes += g.numel() * g.element_size()
+        timed = self.timeline is not None and g.is_cuda and self.info.backend == "nccl"
+        if timed:
+            ready = torch.cuda.Event(enable_timing=True)
+            ready.record()  # compute stream: the bucket's last gradient is written here
         if self.mode == "allreduce":
             self._works.append(dist.all_reduce(g, group=group, async_op=True))
         else:
             a, e = b.piece(rank, world)
             self._works.append(dist.reduce_scatter_tensor(self.store.grads[a:e], g, group=group, async_op=True))
+        if timed:
+            # the collective's completion, seen from an otherwise idle stream: wait() under it makes THAT stream (not
+            # the compute stream) wait for RCCL, and the event behind it fires when the collective is done
+            if self._tl_stream is None:
+                self._tl_stream = torch.cuda.Stream(device=g.device)
+            done = torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(self._tl_stream):
+                self._works[-1].wait()
+                done.record()
+            self._tl_cur.append((b.index, ready, done))
 
     def finish_grads(self) -> None:
         """Make the current (compute) stream wait for every outstanding gradient collective. With
@@ -96,6 +115,9 @@ class DataParallel:
         if timed:
             e1.record()
             self.finish_waits.append((e0, e1))
+            if self.timeline is not None and self._tl_cur:
+                self.timeline.append({"bwd_end": e0, "buckets": list(self._tl_cur)})
+        self._tl_cur.clear()
         self._works.clear()
 
     @property
@@ -174,3 +196,37 @@ class DataParallel:
         for w in self._gather_works:
             w.wait()
         self._gather_works.clear()
+
+
+def timeline_summary(steps: list[dict]) -> dict | None:
+    """Per-rank gradient-collective timeline (bench JSON), from ``DataParallel.timeline`` after a synchronize.
+
+    Times are ms relative to backward's last kernel on the compute stream (negative: before it), medians over the
+    timed steps: when the first / last bucket's gradients were ready, when the first / last collective completed,
+    and the span the collectives were in flight. ``last_done_ms`` > 0 is communication exposed after backward."""
+    rows = []
+    for st in steps:
+        bk = st["buckets"]
+        if not bk:
+            continue
+        ref = bk[0][1]  # the first ready event: everything below is recorded after it
+        t = lambda ev: ref.elapsed_time(ev)  # noqa: E731
+        end = t(st["bwd_end"])
+        ready = [t(r) - end for _, r, _ in bk]
+        done = [t(d) - end for _, _, d in bk]
+        rows.append({"n_buckets": len(bk), "first_ready_ms": min(ready), "last_ready_ms": max(ready),
+                     "first_done_ms": min(done), "last_done_ms": max(done), "in_flight_ms": max(done) - min(ready)})
+    return summarize_rows(rows)
+
+
+def summarize_rows(rows: list[dict]) -> dict | None:
+    """Median of each field over the steps (pure; tests feed it numbers)."""
+    if not rows:
+        return None
+    out = {}
+    for k in rows[0]:
+        v = sorted(r[k] for r in rows)
+        m = v[len(v) // 2] if len(v) % 2 else 0.5 * (v[len(v) // 2 - 1] + v[len(v) // 2])
+        out[k] = round(m, 3) if isinstance(m, float) else m
+    out["steps"] = len(rows)
+    return out

@@ -107,34 +107,70 @@ def _read(path: str) -> str:
         return f.read().strip()
 
 
+def plan_rank_cpus(local_rank: int, gpu_cpus: dict[int, list[int]], allowed: set[int]) -> tuple[list[int], str]:
+    """Which CPUs local rank ``local_rank`` should run on, and why (pure: ``bind_rank_cpus`` and the tests use it).
+
+    ``gpu_cpus``: local rank -> its GPU's NUMA-local CPUs (sysfs ``local_cpulist``); ``allowed``: the CPUs this
+    process may use (cgroup / ``sched_getaffinity``). The ranks whose GPUs share one NUMA CPU list split it evenly
+    (in local-rank order); the rank takes its share intersected with ``allowed``. When that is empty (a cgroup that
+    leaves this NUMA node's share out) it falls back to every allowed CPU of its NUMA node, then to the allowed CPUs
+    split evenly over all local ranks -- never to nothing, and the reason says which."""
+    cpus = gpu_cpus[local_rank]
+    peers = sorted(r for r, c in gpu_cpus.items() if c == cpus)
+    k, n = peers.index(local_rank), len(peers)
+    share = cpus[k * len(cpus) // n:(k + 1) * len(cpus) // n]
+    want = [c for c in share if c in allowed]
+    if want:
+        return want, f"numa share {k + 1}/{n}"
+    want = [c for c in cpus if c in allowed]
+    if want:
+        return want, "numa share not allowed: all allowed cpus of the numa node"
+    al = sorted(allowed)
+    ranks = sorted(gpu_cpus)
+    k, n = ranks.index(local_rank), len(ranks)
+    want = al[k * len(al) // n:(k + 1) * len(al) // n] or al
+    return want, "no numa-local cpu allowed: even split of the allowed cpus"
+
+
+def rank_threads(ncpus_bound: int | None, nallowed: int, local_world: int) -> int:
+    """Intra-op threads per rank: the CPUs the rank is bound to, else an even share of the allowed ones (never the
+    box's whole count per rank: 8 ranks x OMP_NUM_THREADS=16 on a 16-CPU share oversubscribes 8x)."""
+    if ncpus_bound:
+        return max(1, ncpus_bound)
+    return max(1, nallowed // max(1, local_world))
+
+
+def _fmt_cpus(want: list[int]) -> str:
+    return f"{want[0]}-{want[-1]}" if want == list(range(want[0], want[-1] + 1)) else ",".join(map(str, want))
+
+
 def bind_rank_cpus(info: DistInfo) -> dict | None:
-    """Pin this rank to the CPUs next to its GPU: the GPU's sysfs ``local_cpulist`` (its NUMA node), split
-    evenly among the local ranks whose GPUs share that list, intersected with the CPUs this process may use.
-    Multi-rank GPU jobs only (the one-GPU headline runs unpinned); ``KOP_CPU_AFFINITY=0`` turns it off.
-    Returns {"numa_node", "cpus"} (what was bound) or None."""
-    if info.device.type != "cuda" or info.world <= 1 or os.environ.get("KOP_CPU_AFFINITY", "1") == "0":
-        return None
-    try:
-        mine = _gpu_pci_dir(info.local_rank)
-        cpus = parse_cpulist(_read(mine + "/local_cpulist"))
-        numa = int(_read(mine + "/numa_node"))
-        nloc = int(os.environ.get("LOCAL_WORLD_SIZE", torch.cuda.device_count()))
-        peers = [i for i in range(min(nloc, torch.cuda.device_count()))
-                 if parse_cpulist(_read(_gpu_pci_dir(i) + "/local_cpulist")) == cpus]
-    except (OSError, ValueError, RuntimeError):
+    """Pin this rank to the CPUs next to its GPU (``plan_rank_cpus``) and size torch's intra-op thread pool to them
+    (``rank_threads``). Multi-rank GPU jobs only (the one-GPU headline runs unpinned); ``KOP_CPU_AFFINITY=0`` turns
+    the pinning off (the thread count is still set). Returns what was done and why, for the bench JSON:
+    {"rank", "gpu", "numa_node", "cpus", "ncpus", "allowed", "threads", "reason"} (None: one rank / CPU)."""
+    if info.device.type != "cuda" or info.world <= 1:
         return None
     allowed = os.sched_getaffinity(0)
-    if info.local_rank in peers and len(peers) > 1:
-        k, n = peers.index(info.local_rank), len(peers)
-        share = cpus[k * len(cpus) // n:(k + 1) * len(cpus) // n]
+    nloc = int(os.environ.get("LOCAL_WORLD_SIZE", torch.cuda.device_count()))
+    rec = {"rank": info.rank, "gpu": info.local_rank, "numa_node": None, "cpus": None, "ncpus": 0,
+           "allowed": len(allowed), "threads": None, "reason": ""}
+    if os.environ.get("KOP_CPU_AFFINITY", "1") == "0":
+        rec["reason"] = "KOP_CPU_AFFINITY=0: unpinned"
     else:
-        share = cpus
-    want = [c for c in share if c in allowed] or [c for c in cpus if c in allowed]
-    if not want:
-        return None
-    os.sched_setaffinity(0, want)
-    return {"numa_node": numa, "cpus": f"{want[0]}-{want[-1]}" if want == list(range(want[0], want[-1] + 1))
-            else ",".join(map(str, want)), "ncpus": len(want)}
+        try:
+            ndev = min(nloc, torch.cuda.device_count())
+            gpu_cpus = {i: parse_cpulist(_read(_gpu_pci_dir(i) + "/local_cpulist")) for i in range(ndev)}
+            rec["numa_node"] = int(_read(_gpu_pci_dir(info.local_rank) + "/numa_node"))
+            want, rec["reason"] = plan_rank_cpus(info.local_rank, gpu_cpus, allowed)
+            os.sched_setaffinity(0, want)
+            rec["cpus"], rec["ncpus"] = _fmt_cpus(want), len(want)
+        except (OSError, ValueError, RuntimeError, KeyError) as e:
+            rec["reason"] = f"unpinned: {type(e).__name__}: {e}"[:160]
+    rec["threads"] = rank_threads(rec["ncpus"], len(allowed), nloc)
+    torch.set_num_threads(rec["threads"])
+    os.environ["OMP_NUM_THREADS"] = str(rec["threads"])  # for anything this rank starts later
+    return rec
 
 
 def runtime_env() -> dict:
@@ -172,6 +208,15 @@ def all_reduce_sum(x: float, info: DistInfo) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=info.device if info.backend == "nccl" else "cpu")
     dist.all_reduce(t, group=info.group)
     return float(t.item())
+
+
+def gather_objects(obj, info: DistInfo) -> list | None:
+    """Every rank's ``obj`` on every rank (None without collectives)."""
+    if not collectives_on(info):
+        return None
+    out = [None] * dist.get_world_size(info.group)
+    dist.all_gather_object(out, obj, group=info.group)
+    return out
 
 
 def shutdown(info: DistInfo) -> None:

@@ -143,3 +143,56 @@ def test_cpulist_parsing():
 
     assert parse_cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
     assert parse_cpulist("") == []
+
+
+# --- the first 8-GPU run must be attributable -------------------------------------------------
+# an MI355X node as sysfs shows it: GPUs 0-3 on NUMA node 0 (CPUs 0-63), GPUs 4-7 on node 1 (CPUs 64-127)
+_NODE = {i: list(range(0, 64)) if i < 4 else list(range(64, 128)) for i in range(8)}
+
+
+def test_rank_cpu_plan_splits_each_numa_node_and_records_why():
+    from kubeoperator_amd.parallel.dist import plan_rank_cpus
+
+    allowed = set(range(128))
+    plans = [plan_rank_cpus(r, _NODE, allowed) for r in range(8)]
+    assert [p[0][0] for p in plans] == [0, 16, 32, 48, 64, 80, 96, 112]
+    assert all(len(p[0]) == 16 and p[1].startswith("numa share") for p in plans)
+    # a cgroup that grants 16 CPUs of node 0 only (the gpurun box's share): node-0 ranks keep their shares within it,
+    # node-1 ranks cannot get a NUMA-local CPU and split the allowed set evenly -- with the reason recorded
+    allowed = set(range(0, 16))
+    p0 = plan_rank_cpus(0, _NODE, allowed)
+    assert p0 == (list(range(0, 16)), "numa share 1/4")
+    p1 = plan_rank_cpus(1, _NODE, allowed)
+    assert p1[0] == list(range(0, 16)) and p1[1].startswith("numa share not allowed")
+    p5 = plan_rank_cpus(5, _NODE, allowed)
+    assert p5 == ([10, 11], "no numa-local cpu allowed: even split of the allowed cpus")
+    assert all(plan_rank_cpus(r, _NODE, allowed)[0] for r in range(8))  # never an empty CPU set
+
+
+def test_rank_threads_never_oversubscribe(monkeypatch):
+    from kubeoperator_amd.parallel.dist import rank_threads
+
+    assert rank_threads(16, 128, 8) == 16  # pinned: the CPUs it is pinned to
+    assert rank_threads(0, 16, 8) == 2  # unpinned: an even share of the allowed CPUs, not OMP's 16 each
+    assert rank_threads(None, 4, 8) == 1
+
+    # the self-launch hands each child rank an even share of this process's CPUs
+    import bench
+
+    seen = {}
+    monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(16)))
+    monkeypatch.setattr(subprocess, "call", lambda cmd, env=None: seen.update(env=env) or 0)
+    monkeypatch.setenv("OMP_NUM_THREADS", "16")
+    assert bench._self_launch(8) == 0
+    assert seen["env"]["OMP_NUM_THREADS"] == "2"
+
+
+def test_bucket_timeline_summary_is_the_median_over_steps():
+    from kubeoperator_amd.parallel.ddp import summarize_rows
+
+    rows = [{"n_buckets": 3, "first_ready_ms": -40.0 - i, "last_ready_ms": -1.0, "first_done_ms": -30.0,
+             "last_done_ms": 2.0 + i, "in_flight_ms": 42.0} for i in range(3)]
+    s = summarize_rows(rows)
+    assert s == {"n_buckets": 3, "first_ready_ms": -41.0, "last_ready_ms": -1.0, "first_done_ms": -30.0,
+                 "last_done_ms": 3.0, "in_flight_ms": 42.0, "steps": 3}
+    assert summarize_rows([]) is None

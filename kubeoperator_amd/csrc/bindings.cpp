@@ -258,6 +258,30 @@ std::vector<Tensor> cross_entropy_fwd_(const Tensor& logits, const Tensor& targe
   return {loss, lse, scale};
 }
 
+// ------------------------------------------------------------------ embedding gradient
+// out (+)= the embedding weight gradient of (ids, dy), written straight into ``out`` (the flat gradient buffer's view of
+// the table): one stable radix sort of the int32 ids + the run-sum kernel; no dense fp32 scratch
+void embedding_bwd_(const Tensor& ids, const Tensor& dy, const Tensor& out, bool accumulate) {
+  check_gpu(ids, "ids");
+  check_bf16(dy, "dy");
+  check_rows(dy, "dy");
+  check_gpu(out, "out");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat, "out must be bf16 or fp32");
+  TORCH_CHECK(out.dim() == 2 && out.stride(1) == 1 && out.stride(0) % 8 == 0, "out must be [V, H] with contiguous rows");
+  check_aligned(out, "out");
+  TORCH_CHECK(ids.numel() == dy.size(0) && out.size(1) == dy.size(1), "embedding_bwd: shape mismatch");
+  const int64_t T = ids.numel();
+  TORCH_CHECK(T < ((int64_t)1 << 31), "embedding_bwd: too many tokens");
+  if (!accumulate) out.zero_();
+  if (T == 0) return;
+  auto sr = at::sort(ids.reshape({-1}).to(at::kInt), /*stable=*/true, /*dim=*/0, /*descending=*/false);
+  const Tensor& sid = std::get<0>(sr);
+  const Tensor& perm = std::get<1>(sr);
+  rc(kop::embedding_bwd(sid.data_ptr<int>(), perm.data_ptr<int64_t>(), bp(dy), dy.stride(0), out.data_ptr(),
+                        out.scalar_type() == at::kFloat, out.stride(0), (int)T, (int)dy.size(1), accumulate, cur_stream()),
+     "embedding_bwd (H a multiple of 8)");
+}
+
 // ------------------------------------------------------------------ transpose
 void transpose_(const Tensor& in, const Tensor& out) {
   check_bf16(in, "in");
@@ -518,6 +542,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_bwd", &gelu_bwd);
   m.def("cross_entropy_fwd_", &cross_entropy_fwd_);
   m.def("transpose_", &transpose_);
+  m.def("embedding_bwd_", &embedding_bwd_);
   m.def("rope_t_", &rope_t_);
   m.def("splitk_reduce_", &splitk_reduce_);
   m.def("fp8_quant_", &fp8_quant_);

@@ -94,6 +94,10 @@ int flash_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16
                    int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, int64_t dos, int64_t dqs,
                    int64_t dks, int64_t dvs, float scale, bool causal, hipStream_t stream);
 
+// embedding.hip: dW[v] (+)= sum of dy[t] over ids[t] == v, from stably sorted int32 ids + the permutation (runs summed
+// in token order); out [V, ldo] bf16 or fp32, zeroed by the caller when not accumulating
+int embedding_bwd(const int* sorted_ids, const int64_t* perm, const bf16_t* dy, int64_t ldy, void* out, bool out_f32,
+                  int64_t ldo, int T, int H, bool accumulate, hipStream_t stream);
 // decode_attn.hip: one query token per sequence against a [B, Hkv, Smax, D] KV cache (lens[b] valid keys),
 // split-K over 256-key chunks; part_o: B * Hq * nsplit * D floats, part_ml: B * Hq * nsplit * 2 floats
 int decode_attn_splits(int max_len);

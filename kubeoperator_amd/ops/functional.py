@@ -57,8 +57,14 @@ def _lib():
 SIDE_LAG_CYCLES = int(os.environ.get("KOP_SIDE_LAG_CYCLES", "0"))
 
 
-def _sink(w: torch.Tensor, produce, *inputs):
-    """``produce(out, accumulate)`` writes the gradient of ``w``; returns what autograd should receive."""
+def _sink(w: torch.Tensor, produce, *inputs, defer: bool = False):
+    """``produce(out, accumulate)`` writes the gradient of ``w``; returns what autograd should receive.
+
+    ``defer``: with the side stream on and a later micro-batch to come (``FlatParamStore.defer_ok``), only the
+    bookkeeping happens now (accumulate flag, readiness, an event marking the inputs ready on the compute stream) and
+    the launches are issued by ``FlatParamStore.run_deferred`` after the NEXT micro-batch's forward has been queued:
+    a gradient whose host-side launch sequence is long (the embedding's sort + run sum) then no longer holds the host
+    while the compute stream runs dry at the micro-batch boundary."""
     mg = getattr(w, "main_grad", None)
     if mg is None:
         g = torch.empty_like(w)
@@ -66,6 +72,25 @@ def _sink(w: torch.Tensor, produce, *inputs):
         return g
     hooks = w._kop_hooks
     acc = hooks.accumulate_for(w)
+    store = hooks.store
+    if defer and store.wgrad_stream and store.defer_ok and mg.is_cuda and not torch.cuda.is_current_stream_capturing():
+        ready = torch.cuda.Event()
+        ready.record()
+
+        def launch():
+            side = store.side_stream()
+            side.wait_event(ready)
+            with torch.cuda.stream(side):
+                if SIDE_LAG_CYCLES > 0:
+                    torch.cuda._sleep(SIDE_LAG_CYCLES)
+                produce(mg, acc)
+            for t in inputs:
+                t.record_stream(side)
+            store.hold_side(inputs)
+
+        store.defer(launch)
+        hooks.ready(w)
+        return None
     if hooks.store.wgrad_stream and mg.is_cuda and not torch.cuda.is_current_stream_capturing():
         store = hooks.store
         side = store.side_stream()
@@ -820,6 +845,9 @@ def rope_positions_(x, cos, sin, pos, nheads, D):
 # ---------------------------------------------------------------------------------------------------
 # embedding
 # ---------------------------------------------------------------------------------------------------
+_EMB_HIP = os.environ.get("KOP_EMB_BWD", "hip") == "hip"
+
+
 class _Embedding(Function):
     @staticmethod
     def forward(ctx, ids, w):
@@ -833,9 +861,19 @@ class _Embedding(Function):
         (ids,) = ctx.saved_tensors
         w = ctx.w
         H = w.shape[1]
+        dy2 = dy.reshape(-1, H)
+        if _EMB_HIP and dy2.is_cuda and dy2.dtype == torch.bfloat16 and H % 8 == 0:
+            # csrc/embedding.hip: one stable sort of the ids + a run-sum kernel straight into the gradient buffer (no
+            # dense fp32 [V, H] scratch, no fill / copy of the whole table)
+            dy2 = dy2.contiguous()
+
+            def prod(out, acc):
+                _lib().embedding_bwd_(ids.reshape(-1), dy2, out.view(-1, H), acc)
+
+            return None, _sink(w, prod, dy2, ids, defer=True)
 
         def prod(out, acc):
-            g = torch.ops.aten.embedding_dense_backward(dy.reshape(-1, H), ids.reshape(-1), ctx.V, -1, False)
+            g = torch.ops.aten.embedding_dense_backward(dy2, ids.reshape(-1), ctx.V, -1, False)
             if acc:
                 out.add_(g)
             else:

@@ -26,6 +26,7 @@ streams underneath the compute-bound forward GEMMs of step k+1 instead of runnin
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -156,6 +157,10 @@ class FlatParamStore:
         self._used: set[int] = set()
         self._side = None  # weight-gradient stream (ops.functional._sink)
         self._held: list = []  # (event, tensors) the side stream still reads (hold_side)
+        # side-stream gradient launches deferred past the next micro-batch's forward (ops.functional._sink(defer=True));
+        # allowed only while a later micro-batch of the step follows (the trainer sets defer_ok)
+        self._deferred: list = []
+        self.defer_ok = False
         self.gate_waits: list | None = None  # (event, event) around collective-gate waits (exposed comm timing)
         self.wgrad_stream = False  # issue weight gradients on it (set by the trainer)
         name_to_bucket = {nm: b for b in self.buckets for nm in b.names}
@@ -245,7 +250,10 @@ class FlatParamStore:
     # weight-gradient stream ---------------------------------------------------------------------
     def side_stream(self):
         if self._side is None:
-            self._side = torch.cuda.Stream(device=self.device)
+            # KOP_SIDE_PRIORITY: HIP stream priority of the weight-gradient stream (lower value = higher priority;
+            # torch.cuda.Stream.priority_range()); 0 = the compute stream's own priority
+            prio = int(os.environ.get("KOP_SIDE_PRIORITY", "0"))
+            self._side = torch.cuda.Stream(device=self.device, priority=prio)
         return self._side
 
     def hold_side(self, tensors) -> None:
@@ -259,9 +267,21 @@ class FlatParamStore:
             held.pop(0)
         held.append((ev, tuple(tensors)))
 
+    def defer(self, launch) -> None:
+        """Queue a side-stream gradient launch for ``run_deferred`` (ops.functional._sink(defer=True))."""
+        self._deferred.append(launch)
+
+    def run_deferred(self) -> None:
+        """Issue the deferred side-stream gradient launches (the trainer calls this once the next micro-batch's forward
+        is queued; ``join_side`` flushes whatever is left)."""
+        pending, self._deferred = self._deferred, []
+        for launch in pending:
+            launch()
+
     def join_side(self) -> None:
         """The compute stream waits for every weight gradient issued on the side stream (end of backward);
         from here on every compute-stream write is ordered after the side stream's reads."""
+        self.run_deferred()
         if self._side is not None:
             torch.cuda.current_stream().wait_stream(self._side)
         self._held.clear()

@@ -145,7 +145,11 @@ class Trainer:
             if graphed:
                 losses.append(self._replay(min(i, 1), ids, tgt))
                 continue
+            # a gradient launch deferred by the previous micro-batch's backward (_sink(defer=True)) goes out now,
+            # behind this micro-batch's queued forward; none is deferred out of the last micro-batch
+            self.store.defer_ok = i < n - 1
             loss = self.model(ids, tgt)
+            self.store.run_deferred()
             loss.backward()
             losses.append(loss.detach())
         self.store.join_side()

@@ -65,15 +65,23 @@ def split_ref(ref: str) -> tuple[str, str] | None:
 
 
 class OCILayout:
-    """An OCI image layout on disk, indexed by repository name and tag."""
+    """An OCI image layout on disk, indexed by repository name and tag.
+
+    ``index.json`` must be replaced by an atomic rename (write a temporary file, ``os.replace``): a reload parses the
+    new index completely, builds the tag, reachability and media-type tables aside and swaps all three in at once; an
+    index that does not parse (caught mid-write) leaves the previous tables in place and is re-read on the next
+    request."""
 
     def __init__(self, root: str):
         self.root = root
         self.tags: dict[str, dict[str, dict]] = {}  # name -> tag -> descriptor
-        self.reachable: dict[str, set[str]] = {}  # name -> manifest / index digests pullable by digest
+        # name -> every digest a client may pull under that name: manifests / indexes (by digest) and the config and
+        # layer blobs they reference -- a blob of another repository is refused (BLOB_UNKNOWN)
+        self.reachable: dict[str, set[str]] = {}
         self.media: dict[str, str] = {}  # manifest digest -> media type
         self._hash_cache: dict[str, tuple[int, float, str]] = {}
         self._hash_lock = threading.Lock()
+        self._hashing: dict[str, threading.Event] = {}  # blob path -> set when its in-flight hash is done
         self._load_lock = threading.Lock()
         self._index_mtime = None
         self.load()
@@ -87,7 +95,11 @@ class OCILayout:
         if m != self._index_mtime:
             with self._load_lock:
                 if m != self._index_mtime:
-                    self.load()
+                    try:
+                        self.load()
+                    except (OSError, ValueError) as e:  # mid-write: keep serving the old index, retry next request
+                        log.warning("registry %s: index.json not loadable yet (%s); keeping the previous index",
+                                    self.root, e)
 
     def blob_path(self, digest: str) -> str:
         algo, _, hexd = digest.partition(":")
@@ -95,16 +107,18 @@ class OCILayout:
 
     def load(self) -> None:
         path = os.path.join(self.root, "index.json")
-        self._index_mtime = os.stat(path).st_mtime_ns
+        m = os.stat(path).st_mtime_ns
         with open(path) as f:
-            index = json.load(f)
+            index = json.load(f)  # parse first: a failure leaves every table (and the recorded mtime) as it was
         # build the new tables aside, then swap them in: a request in flight sees the old or the new index, whole
         tags: dict[str, dict[str, dict]] = {}
         reach: dict[str, set[str]] = {}
-        self._index(index, tags, reach)
-        self.tags, self.reachable = tags, reach
+        media: dict[str, str] = {}
+        self._index(index, tags, reach, media)
+        self.tags, self.reachable, self.media = tags, reach, media
+        self._index_mtime = m
 
-    def _index(self, index: dict, tags: dict, reach: dict) -> None:
+    def _index(self, index: dict, tags: dict, reach: dict, media: dict) -> None:
         for d in index.get("manifests", []):
             ann = d.get("annotations") or {}
             parsed = None
@@ -117,49 +131,77 @@ class OCILayout:
                 continue
             name, tag = parsed
             tags.setdefault(name, {})[tag] = d
-            self.media[d["digest"]] = d.get("mediaType", OCI_MANIFEST)
-            self._walk(name, d["digest"], reach)
+            media[d["digest"]] = d.get("mediaType", OCI_MANIFEST)
+            self._walk(name, d["digest"], reach, media)
 
-    def _walk(self, name: str, digest: str, reach: dict) -> None:
+    def _walk(self, name: str, digest: str, reach: dict, media: dict) -> None:
         seen = reach.setdefault(name, set())
         if digest in seen:
             return
         seen.add(digest)
-        if self.media.get(digest) in INDEX_TYPES:
-            try:
-                with open(self.blob_path(digest), "rb") as f:
-                    body = json.load(f)
-            except (OSError, ValueError):
-                return
+        kind = media.get(digest)
+        if kind not in INDEX_TYPES and kind not in MANIFEST_TYPES:
+            return  # a config or layer blob
+        try:
+            with open(self.blob_path(digest), "rb") as f:
+                body = json.load(f)
+        except (OSError, ValueError):
+            return
+        if kind in INDEX_TYPES:
             for child in body.get("manifests", []):
                 if _DIGEST_RE.match(child.get("digest", "")):
-                    self.media[child["digest"]] = child.get("mediaType", OCI_MANIFEST)
-                    self._walk(name, child["digest"], reach)
+                    media[child["digest"]] = child.get("mediaType", OCI_MANIFEST)
+                    self._walk(name, child["digest"], reach, media)
+            return
+        for desc in [body.get("config") or {}] + list(body.get("layers") or []):
+            if _DIGEST_RE.match(desc.get("digest", "")):
+                seen.add(desc["digest"])
 
     def verified_digest(self, digest: str) -> bool:
-        """True if the blob file exists and hashes to ``digest`` (hash cached by size + mtime)."""
+        """True if the blob file exists and hashes to ``digest`` (hash cached by size + mtime). One thread hashes a
+        given blob at a time: concurrent requests for a blob that is being hashed (many nodes pulling the same
+        multi-GB layer at once) wait for that result instead of each reading and hashing the whole file."""
         p = self.blob_path(digest)
-        try:
-            st = os.stat(p)
-        except OSError:
-            return False
-        with self._hash_lock:
-            c = self._hash_cache.get(p)
-        if c is None or c[0] != st.st_size or c[1] != st.st_mtime:
-            h = hashlib.sha256()
-            with open(p, "rb") as f:
-                for chunk in iter(lambda: f.read(1 << 20), b""):
-                    h.update(chunk)
-            c = (st.st_size, st.st_mtime, "sha256:" + h.hexdigest())
+        while True:
+            try:
+                st = os.stat(p)
+            except OSError:
+                return False
             with self._hash_lock:
-                self._hash_cache[p] = c
-        return c[2] == digest
+                c = self._hash_cache.get(p)
+                if c is not None and c[0] == st.st_size and c[1] == st.st_mtime:
+                    return c[2] == digest
+                busy = self._hashing.get(p)
+                if busy is None:
+                    mine = self._hashing[p] = threading.Event()
+            if busy is not None:
+                busy.wait()
+                continue  # re-check the cache the hashing thread filled (or hash it now if it failed)
+            try:
+                h = hashlib.sha256()
+                with open(p, "rb") as f:
+                    for chunk in iter(lambda: f.read(1 << 20), b""):
+                        h.update(chunk)
+                c = (st.st_size, st.st_mtime, "sha256:" + h.hexdigest())
+                with self._hash_lock:
+                    self._hash_cache[p] = c
+                return c[2] == digest
+            except OSError:
+                return False
+            finally:
+                with self._hash_lock:
+                    self._hashing.pop(p, None)
+                mine.set()
+
+    def blob_reachable(self, name: str, digest: str) -> bool:
+        return digest in self.reachable.get(name, ())
 
     def resolve_manifest(self, name: str, ref: str) -> str | None:
         if name not in self.tags:
             return None
         if _DIGEST_RE.match(ref):
-            return ref if ref in self.reachable.get(name, ()) else None
+            # a manifest / index of this repository (its config and layer digests are reachable too, as blobs only)
+            return ref if ref in self.reachable.get(name, ()) and ref in self.media else None
         d = self.tags[name].get(ref)
         return d["digest"] if d else None
 
@@ -252,7 +294,8 @@ class _RegistryHandler(http.server.BaseHTTPRequestHandler):
     def _blob(self, name: str, digest: str, head: bool) -> None:
         if not _DIGEST_RE.match(digest):
             return self._error(400, "DIGEST_INVALID", f"invalid digest {digest}", head)
-        if not self.layout.verified_digest(digest):
+        # only blobs an image of THIS repository references (distribution spec: a blob is scoped to its repository)
+        if not self.layout.blob_reachable(name, digest) or not self.layout.verified_digest(digest):
             return self._error(404, "BLOB_UNKNOWN", f"blob unknown to registry: {digest}", head)
         p = self.layout.blob_path(digest)
         size = os.path.getsize(p)

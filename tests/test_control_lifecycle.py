@@ -209,6 +209,19 @@ def test_full_lifecycle(control):
     assert not [c for _, c in farm.log if re.search(r"\{\{\s*[A-Za-z_]|\{%", c)]
     cfg = farm.fs["w1"]["/etc/containerd/config.toml"].decode()
     assert re.search(r'^root = "/[^"{]+"$', cfg, re.M) and 'sandbox_image = "' in cfg
+    # GPU repositories only on GPU nodes (a package without a GPU tree must not break apt on the others)
+    src_m1 = farm.fs["m1"]["/etc/apt/sources.list.d/kubeoperator.list"].decode()
+    src_w1 = farm.fs["w1"]["/etc/apt/sources.list.d/kubeoperator.list"].decode()
+    assert "/rocm/" not in src_m1 and "/amdgpu/" not in src_m1
+    assert "/rocm/apt/7.0 " in src_w1 and "/amdgpu/apt/7.0.70000-1 " in src_w1
+    assert any("/amdgpu/apt/7.0.70000-1/Packages" in c for c in farm.commands("w1"))  # preflight checked the tree
+    # registry hosts in the config_path form containerd 2.x requires (no deprecated registry.mirrors table)
+    assert 'config_path = "/etc/containerd/certs.d"' in cfg and "registry.mirrors" not in cfg
+    hosts = {p: d.decode() for p, d in farm.fs["w1"].items() if p.startswith("/etc/containerd/certs.d/")}
+    assert {"/etc/containerd/certs.d/docker.io/hosts.toml", "/etc/containerd/certs.d/registry.k8s.io/hosts.toml"} <= set(hosts)
+    for body in hosts.values():
+        srv = re.search(r'^server = "(http://[^"]+)"$', body, re.M).group(1)
+        assert f'[host."{srv}"]' in body and 'capabilities = ["pull", "resolve"]' in body
 
     assert deploy.create("demo", "gpu-validate", run="inline")["state"] == "SUCCESS"
 

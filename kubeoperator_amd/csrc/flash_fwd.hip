@@ -518,6 +518,12 @@ int flash_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o,
   const int env_variant = flash_attn_set_fwd_variant(-3);  // current setting (-3 changes nothing)
   int variant = env_variant >= 0 ? env_variant : (D == 64 && causal) ? 0 : 8;
   if (ot != nullptr && variant < 8) variant = 8;  // O^T comes only from the 8-wave kernel
+  // 12: the 4-wave one-wave-per-SIMD kernel, 64 rows per wave, hand-scheduled double pipeline (csrc/flash_fwd4.hip;
+  // D = 128). An 8-wave double pipeline (QK of tile t+1 beside the softmax of tile t, 2 waves per SIMD) ran 15 %
+  // slower and spilled: profiles/r5_experiments.md
+  if (S % 256 == 0 && variant == 12 && D == 128) {
+    return flash_attn_fwd4x64(q, k, v, o, lse, B, S, Hq, Hkv, D, qs, ks, vs, os, sl2, causal, stream, ot);
+  }
   if (S % 256 == 0 && variant >= 8) {
     if (D == 128) {
       if (variant == 9) launch_fwd8<128, true>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream, ot);

@@ -70,6 +70,10 @@ int fp8_transpose_cast(const bf16_t* in, uint8_t* out, int64_t R, int64_t C, int
 int flash_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int S, int Hq,
                    int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, float scale, bool causal,
                    hipStream_t stream, bf16_t* ot = nullptr);
+// 4-wave one-wave-per-SIMD forward (csrc/flash_fwd4.hip); sl2 = scale * log2(e); S % 256 == 0, D 64 / 128
+int flash_attn_fwd4x64(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int S, int Hq,
+                       int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, float sl2, bool causal,
+                       hipStream_t stream, bf16_t* ot);
 size_t flash_attn_bwd_workspace(int B, int S, int Hq, int D);
 // dQ algorithm: 10 = from the materialised dS (default), 9 = recompute S/dP (8-wave, staggered),
 // 8 = lockstep, <8 = 4-wave.

@@ -60,7 +60,8 @@ def _run(cmd: list[str]) -> None:
 
 # per-file hipcc flags: the one-wave-per-SIMD dK/dV kernel keeps its builtin MFMAs in VGPR form (its dK/dV
 # accumulators are AGPR inline-asm operands; hipcc's heuristic would put every MFMA in AGPR form)
-FILE_FLAGS = {"flash_bwd_w1.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=true"]}
+FILE_FLAGS = {"flash_bwd_w1.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=true"],
+              "flash_fwd4.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=true", "-fno-slp-vectorize", "-fno-honor-nans"]}
 
 
 def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -> str:

@@ -1,0 +1,72 @@
+// Stand-alone cycle probe of the hand-scheduled attention forward (csrc/flash_fwd4.hip) at the Llama-3-8B shape
+// (B 1, S 8192, 32 / 8 heads, D 128): kernel time by events, plus per-segment s_memtime stamps summed over the waves
+// (KOP_FWD4_STAMP: top-of-tile DMA wait + barrier, the scheduled 64-MFMA tile, the unscheduled diagonal / last tiles,
+// epilogue). Build / run:
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form=true -I kubeoperator_amd/csrc \
+//         tools/fwd4_probe.hip -o tools/bin/fwd4_probe && tools/bin/fwd4_probe
+#define KOP_FWD4_STAMP 1
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../kubeoperator_amd/csrc/flash_fwd4.hip"
+
+using namespace kop;
+
+int main() {
+  const int B = 1, S = 8192, Hq = 32, Hkv = 8, Dh = 128;
+  const int C = (Hq + 2 * Hkv) * Dh;
+  const size_t nqkv = (size_t)B * S * C;
+  std::vector<uint16_t> h(nqkv);
+  uint32_t x = 12345;
+  for (auto& e : h) {  // bf16 ~ N(0, 1)-ish: sum of uniforms
+    float f = 0.f;
+    for (int i = 0; i < 4; ++i) {
+      x = x * 1664525u + 1013904223u;
+      f += (x >> 8) * (1.f / 16777216.f) - 0.5f;
+    }
+    f *= 1.7f;
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    e = (uint16_t)((u + 0x7fff + ((u >> 16) & 1)) >> 16);
+  }
+  bf16_t *qkv, *o;
+  float* lse;
+  (void)hipMalloc(&qkv, nqkv * 2);
+  (void)hipMalloc(&o, (size_t)B * S * Hq * Dh * 2);
+  (void)hipMalloc(&lse, (size_t)B * Hq * S * 4);
+  (void)hipMemcpy(qkv, h.data(), nqkv * 2, hipMemcpyHostToDevice);
+  const float sl2 = 1.4426950408889634f / sqrtf((float)Dh);
+  for (int causal = 1; causal >= 0; --causal) {
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    for (int w = 0; w < 3; ++w)
+      flash_attn_fwd4x64(qkv, qkv + Hq * Dh, qkv + (Hq + Hkv) * Dh, o, lse, B, S, Hq, Hkv, Dh, C, C, C, Hq * Dh, sl2,
+                         causal, 0, nullptr);
+    unsigned long long z[12] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fwd4_stamp), z, sizeof(z));
+    const int iters = 10;
+    (void)hipEventRecord(e0, 0);
+    for (int i = 0; i < iters; ++i)
+      flash_attn_fwd4x64(qkv, qkv + Hq * Dh, qkv + (Hq + Hkv) * Dh, o, lse, B, S, Hq, Hkv, Dh, C, C, C, Hq * Dh, sl2,
+                         causal, 0, nullptr);
+    (void)hipEventRecord(e1, 0);
+    (void)hipEventSynchronize(e1);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    unsigned long long st[12];
+    (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(g_fwd4_stamp), sizeof(st));
+    const double flops = 4.0 * B * Hq * (double)S * S * Dh * (causal ? 0.5 : 1.0);
+    const double ns = st[3] ? (double)st[3] : 1.0, np = st[4] ? (double)st[4] : 1.0;
+    const double tiles = ns + np;
+    printf("{\"causal\": %d, \"ms\": %.4f, \"tflops\": %.1f, \"waves\": %llu, \"sched_tiles\": %llu, \"plain_tiles\": "
+           "%llu, \"cyc_wait_per_tile\": %.0f, \"cyc_sched_per_tile\": %.0f, \"cyc_plain_per_tile\": %.0f, "
+           "\"cyc_loop_per_wave\": %.0f, \"cyc_epilogue_per_wave\": %.0f, \"sched_pre\": %.0f, \"sched_qk\": %.0f, "
+           "\"sched_pv\": %.0f, \"sched_decide\": %.0f}\n",
+           causal, ms / iters, flops / (ms / iters * 1e-3) * 1e-12, st[7], st[3], st[4], st[0] / tiles, st[1] / ns,
+           st[2] / np, (double)st[5] / st[7], (double)st[6] / st[7], st[8] / ns, st[9] / ns, st[10] / ns, st[11] / ns);
+  }
+  return 0;
+}

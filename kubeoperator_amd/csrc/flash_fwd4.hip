@@ -43,7 +43,11 @@ namespace kop {
 
 namespace fwd4 {
 
-constexpr int D = 128, NW = 4, BM = 256, BN = 64, ROWB = 2 * D, TILE = BN * ROWB, NSLOT = 3;
+#ifndef KOP_FWD4_RING
+#define KOP_FWD4_RING 3  // LDS ring slots: 3 = DMA two tiles ahead, 4 = three (measured equal: r5_experiments.md)
+#endif
+constexpr int D = 128, NW = 4, BM = 256, BN = 64, ROWB = 2 * D, TILE = BN * ROWB, NSLOT = KOP_FWD4_RING;
+constexpr int AHEAD = NSLOT - 1;  // tiles the LDS-DMA runs ahead of the tile being consumed
 constexpr int PPW = (TILE / 1024) / NW;  // LDS-DMA pieces per wave per tile, each of K and V
 constexpr int DT = D / 32, NR = 2 * DT, NK = D / 16, NG = D / 32;
 constexpr int RB = ROWB * 8;
@@ -61,7 +65,8 @@ static_assert(QB(1, NK - 1) + 3 == 255, "O and Q fill a[64:255]");
 constexpr int e_rb(int e) { return e < 16 ? 0 : e < 32 ? 1 : ((e - 32) / 8) & 1; }
 constexpr int e_h(int e) { return e < 32 ? 0 : 1; }
 constexpr int e_j(int e) { return e < 32 ? (e & 15) : (e < 48 ? (e & 7) : 8 + (e & 7)); }
-constexpr int e_slot(int e) { return e * 7 / 8; }  // slots 0..55, 1-2 per slot
+// slots 0..55: one per slot in the QK half (it also carries the LDS-DMA), 1-2 per slot in the P.V half
+constexpr int e_slot(int e) { return e < 24 ? e : 24 + (e - 24) * 32 / 40; }
 // In-order issue stalls on a dependent operand, so each element is software-pipelined over the slots (an MFMA's
 // 32 cycles between stages): v_fma (argument) at e_slot - 2, v_exp at e_slot - 1, the row-sum add at e_slot + 1;
 // slot -1 is the preamble before the first MFMA
@@ -208,8 +213,8 @@ __global__ void __launch_bounds__(256, 1) fa_fwd4x64_kernel(const bf16_t* __rest
   auto issue = [&](int t) {
     for (int i = 0; i < 2 * PPW; ++i) piece(t, i);
   };
-  issue(0);
-  if (ntiles > 1) issue(1);
+  static_assert(AHEAD <= 4, "S % 256 == 0 gives ntiles >= 4");
+  for (int t = 0; t < AHEAD; ++t) issue(t);
   static_for<16 * 2 * DT>([&](auto ic) {
     asm volatile("v_accvgpr_write_b32 a[%0], 0" ::"n"(ABASE + decltype(ic)::value));
   });
@@ -338,7 +343,7 @@ __global__ void __launch_bounds__(256, 1) fa_fwd4x64_kernel(const bf16_t* __rest
 #endif
     float mx[2];
     const float nm0 = -m[0], nm1 = -m[1];
-    const int t2src = t + 2 < ntiles ? t + 2 : ntiles - 1, t2slot = (t + 2) % NSLOT;
+    const int t2src = t + AHEAD < ntiles ? t + AHEAD : ntiles - 1, t2slot = (t + AHEAD) % NSLOT;
     // the softmax of S(t) and the row max of S(t+1) placed in slot s (-1: preamble)
     auto fillers = [&](auto sc) {
       constexpr int s = decltype(sc)::value;
@@ -405,8 +410,8 @@ __global__ void __launch_bounds__(256, 1) fa_fwd4x64_kernel(const bf16_t* __rest
           vbuf[(ks4 + 1) & 1][i] = vread1(b0, b1, std::integral_constant<int, ks4 + 1>{}, std::integral_constant<int, i>{});
         });
       }
-      // LDS-DMA of tile t+2: 8 pieces in slots 2, 5, ..., 23. Branch-free: past the last tile the last tile is
-      // fetched again into t+2's (dead) slot -- only at t = ntiles - 2, and the next top's vmcnt(0) retires it
+      // LDS-DMA of tile t+AHEAD: 8 pieces in slots 2, 5, ..., 23. Branch-free: past the last tile the last tile
+      // is fetched again into a dead slot (tile t-1's), the loop's exit drains it
       // (address one slot ahead: the DMA would otherwise wait on its own address arithmetic)
       if constexpr (s >= 1 && s <= 22 && (s - 1) % 3 == 0) dsrc = piece_src(t2src, (s - 1) / 3);
       if constexpr (s >= 2 && s <= 23 && (s - 2) % 3 == 0) glds16(dsrc, piece_dst(t2slot, (s - 2) / 3));
@@ -433,8 +438,8 @@ __global__ void __launch_bounds__(256, 1) fa_fwd4x64_kernel(const bf16_t* __rest
   };
 
   f32x16 sa[2][2], sb[2][2];
-  if (ntiles > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");  // Q and tile 0 landed
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // Q and tile 0 landed, tiles 1 .. AHEAD-1 in flight
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW * (AHEAD - 1)) : "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   if (act(0)) {
@@ -449,7 +454,9 @@ __global__ void __launch_bounds__(256, 1) fa_fwd4x64_kernel(const bf16_t* __rest
 #endif
   auto step = [&](int it, f32x16 (&cs)[2][2], f32x16 (&ns)[2][2]) {
     KOP_STAMP(t0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K(it+1) is read this trip
+    // K(it+1) is read this trip: its DMA landed, the AHEAD-2 later tiles' may still fly (every trip issues exactly
+    // one tile's pieces, clamped past the end, so the count holds)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW * (AHEAD - 2)) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     KOP_STAMP(t1);
@@ -466,7 +473,8 @@ __global__ void __launch_bounds__(256, 1) fa_fwd4x64_kernel(const bf16_t* __rest
 #ifdef KOP_FWD4_STAMP
       ++n_plain;
 #endif
-      if (it + 2 < ntiles) issue(it + 2);
+      for (int i = 0; i < 2 * PPW; ++i)
+        piece_at(it + AHEAD < ntiles ? it + AHEAD : ntiles - 1, (it + AHEAD) % NSLOT, i);
       if (act(it + 1)) {
         qk_plain(it + 1, ns);
         softmax_pv_plain(it, cs);
@@ -501,6 +509,7 @@ __global__ void __launch_bounds__(256, 1) fa_fwd4x64_kernel(const bf16_t* __rest
   }
   if (it < ntiles) step(it, sa, sb);
 #endif
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped DMA past the last tile
 #undef KBUF
 #undef VBUF
 #ifdef KOP_FWD4_STAMP

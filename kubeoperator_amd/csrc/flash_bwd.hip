@@ -35,38 +35,62 @@ namespace kop {
 
 // delta[b, h, s] = sum_d dO * O
 // and the dK/dV kernel's accumulator initialisers: nlse = -lse / scale (S = Q.K^T starts there, so
-// p = exp2(c * acc)) and ndelta = -delta (dP starts there) -- no negate / scale VALU per stage
+// p = exp2(c * acc)) and ndelta = -delta (dP starts there) -- no negate / scale VALU per stage.
+// A workgroup owns DROWS consecutive positions s of ONE (b, h): the three [B, Hq, S] fp32 outputs and the lse input
+// are contiguous runs (the token-major order before wrote and read them 4 bytes at a time at a stride of S * 4),
+// each lane group of D/8 lanes reads one 16-byte chunk of its row, and every lane has all of its rows' loads in
+// flight before the first reduction.
+constexpr int kDeltaRows = 64;
 template <int D>
 __global__ void __launch_bounds__(256) fa_bwd_delta_kernel(const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout,
                                                            const float* __restrict__ lse, float* __restrict__ delta,
                                                            float* __restrict__ nlse, float* __restrict__ ndelta,
                                                            float lse_mul, int B, int S, int Hq, int64_t os,
                                                            int64_t dos) {
-  constexpr int LPR = D / 8;  // lanes per row
-  const int64_t rows = (int64_t)B * S * Hq;
-  const int64_t row = (int64_t)blockIdx.x * (256 / LPR) + threadIdx.x / LPR;
-  const int c = threadIdx.x % LPR;
-  float a = 0.f;
-  if (row < rows) {
-    const int64_t t = row / Hq;
-    const int h = (int)(row % Hq);
-    float x[8], y[8];
-    unpack8(*reinterpret_cast<const u32x4*>(o + t * os + h * D + c * 8), x);
-    unpack8(*reinterpret_cast<const u32x4*>(dout + t * dos + h * D + c * 8), y);
+  constexpr int LPR = D / 8;              // lanes per row
+  constexpr int RPI = 256 / LPR;          // rows per pass of the block
+  constexpr int NP = kDeltaRows / RPI;    // passes
+  const int nsb = (S + kDeltaRows - 1) / kDeltaRows;
+  const int bh = blockIdx.x / nsb, s0 = (blockIdx.x % nsb) * kDeltaRows;
+  const int bb = bh / Hq, h = bh % Hq;
+  const int c = threadIdx.x % LPR, r = threadIdx.x / LPR;
+  u32x4 xo[NP], xd[NP];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) a += x[i] * y[i];
+  for (int p = 0; p < NP; ++p) {
+    const int s = s0 + p * RPI + r;
+    if (s < S) {
+      const int64_t t = (int64_t)bb * S + s;
+      xo[p] = *reinterpret_cast<const u32x4*>(o + t * os + h * D + c * 8);
+      xd[p] = *reinterpret_cast<const u32x4*>(dout + t * dos + h * D + c * 8);
+    }
   }
 #pragma unroll
-  for (int off = LPR / 2; off > 0; off >>= 1) a += __shfl_xor(a, off, 64);
-  if (row < rows && c == 0) {
-    const int64_t t = row / Hq;
-    const int h = (int)(row % Hq);
-    const int bb = (int)(t / S), s = (int)(t % S);
-    const int64_t i = ((int64_t)(bb * Hq + h)) * S + s;
-    delta[i] = a;
-    ndelta[i] = -a;
-    nlse[i] = -lse[i] * lse_mul;
+  for (int p = 0; p < NP; ++p) {
+    const int s = s0 + p * RPI + r;
+    float x[8], y[8], a = 0.f;
+    if (s < S) {
+      unpack8(xo[p], x);
+      unpack8(xd[p], y);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a += x[i] * y[i];
+    }
+#pragma unroll
+    for (int off = LPR / 2; off > 0; off >>= 1) a += __shfl_xor(a, off, 64);
+    if (s < S && c == 0) {
+      const int64_t i = (int64_t)bh * S + s;
+      delta[i] = a;
+      ndelta[i] = -a;
+      nlse[i] = -lse[i] * lse_mul;
+    }
   }
+}
+
+template <int D>
+static void launch_delta(const bf16_t* o, const bf16_t* dout, const float* lse, float* delta, float* nlse, float* ndelta,
+                         float lse_mul, int B, int S, int Hq, int64_t os, int64_t dos, hipStream_t stream) {
+  static_assert(kDeltaRows % (256 / (D / 8)) == 0, "whole passes");
+  const int nsb = (S + kDeltaRows - 1) / kDeltaRows;
+  fa_bwd_delta_kernel<D><<<B * Hq * nsb, 256, 0, stream>>>(o, dout, lse, delta, nlse, ndelta, lse_mul, B, S, Hq, os, dos);
 }
 
 // =============================================================================================
@@ -979,9 +1003,7 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
   float* delta = dv_part + T * Hq * D;
   float* nlse = delta + T * Hq;
   float* ndelta = nlse + T * Hq;
-  const int rows_per_block = 256 / (D / 8);
-  fa_bwd_delta_kernel<D><<<(int)((T * Hq + rows_per_block - 1) / rows_per_block), 256, 0, stream>>>(
-      o, dout, lse, delta, nlse, ndelta, 1.f / scale, B, S, Hq, os, dos);
+  launch_delta<D>(o, dout, lse, delta, nlse, ndelta, 1.f / scale, B, S, Hq, os, dos, stream);
   const size_t lds_kv = 32 * NW * (D * 2) + 2 * (2 * 32 * (D * 2) + 1024);
   const size_t lds_q = 4 * 64 * (D * 2);
   static bool attr = false;

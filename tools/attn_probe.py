@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--causal", default="1,0")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tag", default=os.environ.get("KOP_PROBE_TAG", ""))
+    ap.add_argument("--sdpa", action="store_true", help="also time torch SDPA (the ROCm build's flash kernels) on the shape")
     a = ap.parse_args()
     from kubeoperator_amd.ops import load
 
@@ -61,6 +62,20 @@ def main():
             print(json.dumps({"tag": a.tag, "shape": name, "causal": causal, "fwd_ms": round(tf, 4),
                               "fwd_tflops": round(fl / tf / 1e9, 1), "fwd_ot_ms": round(tft, 4), "bwd_ms": round(tb, 4),
                               "bwd_tflops": round(2.5 * fl / tb / 1e9, 1)}), flush=True)
+            if a.sdpa:
+                import torch.nn.functional as F
+
+                rep = Hq // Hkv
+                qh = q.reshape(B, S, Hq, D).transpose(1, 2).contiguous().requires_grad_(True)
+                kh = k.reshape(B, S, Hkv, D).transpose(1, 2).repeat_interleave(rep, 1).contiguous().requires_grad_(True)
+                vh = v.reshape(B, S, Hkv, D).transpose(1, 2).repeat_interleave(rep, 1).contiguous().requires_grad_(True)
+                dh = do.reshape(B, S, Hq, D).transpose(1, 2).contiguous()
+                ts = timeit(lambda: F.scaled_dot_product_attention(qh, kh, vh, is_causal=causal), a.iters)
+                out = F.scaled_dot_product_attention(qh, kh, vh, is_causal=causal)
+                tsb = timeit(lambda: torch.autograd.grad(out, (qh, kh, vh), dh, retain_graph=True), max(3, a.iters // 2))
+                print(json.dumps({"tag": "torch_sdpa", "shape": name, "causal": causal, "fwd_ms": round(ts, 4),
+                                  "fwd_tflops": round(fl / ts / 1e9, 1), "bwd_ms": round(tsb, 4),
+                                  "bwd_tflops": round(2.5 * fl / tsb / 1e9, 1)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -46,6 +46,12 @@ __device__ __forceinline__ void stage_st(const bf16x4* x, uint64_t base, uint32_
 #ifndef KOP_DKDV_SDEPTH
 #define KOP_DKDV_SDEPTH 4  // S-phase row-read depth in k-steps (3: the round-4 form)
 #endif
+#ifndef KOP_DKDV_PDEPTH
+#define KOP_DKDV_PDEPTH 3  // dP-phase dO row-read depth in k-steps (4 measured equal: r5_experiments.md)
+#endif
+#ifndef KOP_DKDV_TDEPTH
+#define KOP_DKDV_TDEPTH 3  // transposed-read ring of the dV / dK phases: TDEPTH - 1 steps ahead (2 in round 4; 4 measured equal)
+#endif
 
 // acc += a . b on the 32x32x16 bf16 MFMA with the accumulator in AGPRs (a dependent chain needs no wait states)
 __device__ __forceinline__ void mfma32_agpr(f32x16& acc, bf16x8 a, bf16x8 b) {
@@ -303,20 +309,21 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(lq[0]), "+v"(lq[1]), "+v"(lq[2]), "+v"(lq[3]) : "n"(2 * KS));
     const f32x16 cl = cat4f(lq);
     f32x16 s0, s1;
-    bf16x8 dof[3];
+    constexpr int PD = KOP_DKDV_PDEPTH, TD = KOP_DKDV_TDEPTH;
+    bf16x8 dof[PD];
     f32x4 ld[4];
     static_for<NK>([&](auto kc) {
       constexpr int kk = decltype(kc)::value;
       bf16x8* cur = gq[kk % KS];
-      // younger than group kk: the next KS - 1 groups, and from step NK-2 on the dP phase's 7 early reads
-      constexpr int younger = 2 * (NK - 1 - kk < KS - 1 ? NK - 1 - kk : KS - 1) + (kk > NK - 3 ? 7 : 0);
+      // younger than group kk: the next KS - 1 groups, and from step NK-2 on the dP phase's 4 + PD early reads
+      constexpr int younger = 2 * (NK - 1 - kk < KS - 1 ? NK - 1 - kk : KS - 1) + (kk > NK - 3 ? 4 + PD : 0);
       asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(cur[0]), "+v"(cur[1]) : "n"(younger));
       s0 = mfma32(cur[0], kf0[kk], kk == 0 ? cl : s0);
       s1 = mfma32(cur[0], cur[1], kk == 0 ? cl : s1);
       if constexpr (kk + KS < NK) grp(std::integral_constant<int, kk + KS>{}, cur);
       if constexpr (kk == NK - 3) {  // the dP phase's first reads fly under the last S MFMAs
         static_for<4>([&](auto g) { ld[decltype(g)::value] = lds_read16f_off<128 + 32 * decltype(g)::value>(ldb); });
-        static_for<3>([&](auto i) { dof[decltype(i)::value] = dor(i); });
+        static_for<PD>([&](auto i) { dof[decltype(i)::value] = dor(i); });
       }
       __builtin_amdgcn_sched_barrier(0);
     });
@@ -328,17 +335,17 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     // transposed-read jobs j = 0..2DT-1 of the dV (dO^T block j) and dK (Q^T block j - DT) phases, in buffers
     // tr3[j % 3], each issued two steps (8 MFMAs, ~256 cycles) before its MFMAs: with one step (one 128-cycle MFMA
     // step) of prefetch the waits sat in the LDS latency
-    bf16x4 tr3[3][4];
+    bf16x4 tr3[TD][4];
     auto job = [&](auto jc) {
       constexpr int j = decltype(jc)::value;
-      if constexpr (j < DT) trr(o0, o1, std::integral_constant<int, j>{}, tr3[j % 3]);
-      else trr(qa0, qa1, std::integral_constant<int, j - DT>{}, tr3[j % 3]);
+      if constexpr (j < DT) trr(o0, o1, std::integral_constant<int, j>{}, tr3[j % TD]);
+      else trr(qa0, qa1, std::integral_constant<int, j - DT>{}, tr3[j % TD]);
     };
     static_for<NK>([&](auto kc) {
       constexpr int kk = decltype(kc)::value;
-      bf16x8& cur = dof[kk % 3];
-      // younger than dO row kk: the next two rows, and from step NK-2 on the dV phase's 8 early transposed reads
-      constexpr int younger = (NK - 1 - kk < 2 ? NK - 1 - kk : 2) + (kk > NK - 3 ? 8 : 0);
+      bf16x8& cur = dof[kk % PD];
+      // younger than dO row kk: the next PD - 1 rows, and from step NK-2 on the dV phase's early transposed reads
+      constexpr int younger = (NK - 1 - kk < PD - 1 ? NK - 1 - kk : PD - 1) + (kk > NK - 3 ? 4 * (TD - 1) : 0);
       if constexpr (kk == 0) {
         asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(ld[0]), "+v"(ld[1]), "+v"(ld[2]), "+v"(ld[3]) : "n"(younger + 1));
         asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(cur) : "n"(younger));
@@ -353,11 +360,8 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
         p0 = mfma32(cur, vf0[kk], p0);
         p1 = mfma32(cur, vf1[kk], p1);
       }
-      if constexpr (kk + 3 < NK) cur = dor(std::integral_constant<int, kk + 3>{});
-      if constexpr (kk == NK - 3) {
-        job(std::integral_constant<int, 0>{});
-        job(std::integral_constant<int, 1>{});
-      }
+      if constexpr (kk + PD < NK) cur = dor(std::integral_constant<int, kk + PD>{});
+      if constexpr (kk == NK - 3) static_for<(TD - 1 < 2 * DT ? TD - 1 : 2 * DT)>([&](auto jc) { job(jc); });
       // this step's slice of the 16 scores per block: EP = 16 / NK elements (2 at D = 128, 4 at D = 64)
       constexpr int EP = 16 / NK;
 #pragma unroll
@@ -411,14 +415,17 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     };
     static_for<DT>([&](auto dtc) {
       constexpr int dt = decltype(dtc)::value;
-      bf16x4* t = tr3[dt % 3];
-      wait_tr<4, 4>(t);  // job dt + 1 may still fly
+      bf16x4* t = tr3[dt % TD];
+      wait_tr<4, 4 * (TD - 2)>(t);  // jobs dt + 1 .. dt + TD - 2 may still fly
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         mfma32_agpr(dv0[dt], cat44(t[2 * s], t[2 * s + 1]), pb0[s]);
         mfma32_agpr(dv1[dt], cat44(t[2 * s], t[2 * s + 1]), pb1[s]);
       }
-      job(std::integral_constant<int, dt + 2>{});  // into job dt - 1's buffer (its MFMAs issued a step ago)
+      // into job dt - 1's buffer (its MFMAs issued a step ago). Only real jobs: an asm read into registers nothing
+      // reads afterwards lets hipcc hand them to other values while the LDS data is still on its way (seen at D = 64,
+      // 2 DT = 4 jobs, with TDEPTH 4: wrong dS)
+      if constexpr (dt + TD - 1 < 2 * DT) job(std::integral_constant<int, dt + TD - 1>{});
       // this step's slice of dS = p * (dP - delta): ED = 16 / DT elements (4 at D = 128, 8 at D = 64); query half
       // hs (elements 8hs .. 8hs+7) is complete -- and stored -- at the step that finishes its element 8hs + 7
       constexpr int ED = 16 / DT;
@@ -471,7 +478,7 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
     };
     static_for<DT>([&](auto dtc) {
       constexpr int dt = decltype(dtc)::value;
-      bf16x4* t = tr3[(DT + dt) % 3];  // job DT + dt
+      bf16x4* t = tr3[(DT + dt) % TD];  // job DT + dt
       bf16x4* xc = (dt & 1) ? xb : xa;
       bf16x4* xp = (dt & 1) ? xa : xb;
       if constexpr (QM && !(DIAG & 1)) {
@@ -481,17 +488,17 @@ __global__ void __launch_bounds__(256, 1) fa_bwd_dkdv64_kernel(
             constexpr int u = decltype(uc)::value;
             stage_st<(dt - 1) * SPI + u, (DIAG & 16) != 0>(xp + 2 * u, dsq0, sqoff);
           });
-      } else if constexpr (dt + 1 < DT) {
-        wait_tr<4, 4>(t);  // job DT + dt + 1 may still fly
       } else {
-        wait_tr<4, 0>(t);
+        // jobs DT + dt + 1 .. min(2 DT - 1, DT + dt + TD - 2) may still fly
+        constexpr int yj = (2 * DT - 1 - (DT + dt)) < (TD - 2) ? (2 * DT - 1 - (DT + dt)) : (TD - 2);
+        wait_tr<4, 4 * yj>(t);
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         mfma32_agpr(dk0[dt], cat44(t[2 * s], t[2 * s + 1]), sb0[s]);
         mfma32_agpr(dk1[dt], cat44(t[2 * s], t[2 * s + 1]), sb1[s]);
       }
-      if constexpr (DT + dt + 2 < 2 * DT) job(std::integral_constant<int, DT + dt + 2>{});
+      if constexpr (DT + dt + TD - 1 < 2 * DT) job(std::integral_constant<int, DT + dt + TD - 1>{});
       if constexpr (KT && !(DIAG & 1)) {
         // the 4 dS stores spread over the dK steps (each blocks its wave while the CU's store path takes its 1 KB;
         // bunched 2 + 2 in the dV phase they were exposed): store u = (key block u & 1, query half u >> 1)

@@ -25,6 +25,10 @@
 #include "attn_common.h"
 #include "kernels.h"
 
+#ifndef KOP_FWD8_KDEPTH
+#define KOP_FWD8_KDEPTH 2
+#endif
+
 namespace kop {
 
 template <int D, int NW>
@@ -299,19 +303,20 @@ __global__ void __launch_bounds__(512, 1) fa_fwd8_kernel(const bf16_t* __restric
     const uint32_t k0 = lds_addr(Kb) + kb_lane0, k1 = lds_addr(Kb) + kb_lane1;
     s0 = f32x16{0};
     s1 = f32x16{0};
-    bf16x8 ga[4], gb[4];
-    kgroup(k0, k1, std::integral_constant<int, 0>{}, ga);
-    if constexpr (NG > 1) kgroup(k0, k1, std::integral_constant<int, 1>{}, gb);
+    // K row groups KG deep (KOP_FWD8_KDEPTH; 2 = the round-4 form)
+    constexpr int KG = KOP_FWD8_KDEPTH < NG ? KOP_FWD8_KDEPTH : NG;
+    bf16x8 gk[KG][4];
+    static_for<KG>([&](auto i) { kgroup(k0, k1, i, gk[decltype(i)::value]); });
     static_for<NG>([&](auto gc) {
       constexpr int g = decltype(gc)::value;
-      bf16x8* cur = (g & 1) ? gb : ga;
-      if constexpr (g + 1 < NG) wait_rows4<4>(cur);
-      else wait_rows4<0>(cur);
+      bf16x8* cur = gk[g % KG];
+      constexpr int younger = 4 * (NG - 1 - g < KG - 1 ? NG - 1 - g : KG - 1);
+      wait_rows4<younger>(cur);
       s0 = mfma32(cur[0], qf[2 * g], s0);
       s1 = mfma32(cur[1], qf[2 * g], s1);
       s0 = mfma32(cur[2], qf[2 * g + 1], s0);
       s1 = mfma32(cur[3], qf[2 * g + 1], s1);
-      if constexpr (g + 2 < NG) kgroup(k0, k1, std::integral_constant<int, g + 2>{}, cur);
+      if constexpr (g + KG < NG) kgroup(k0, k1, std::integral_constant<int, g + KG>{}, cur);
     });
     const int kv0 = t * BN;
     if (causal && kv0 + BN - 1 > q0w) {

@@ -7,6 +7,10 @@ with a progress line per shape (a long silent tuning run looks hung to the job r
    trainer load read-only (``--gemm-tuning use``).
 
 Usage (one MI355X): python tools/tune_gemms.py [--model llama3_8b --seq 8192 --mbs 1]
+Re-tune under other settings into a separate file (A/B against the committed winners with KOP_GEMM_RESULTS=<out>):
+  KOP_TUNE_MS=200 KOP_TUNE_ITERS=100 python tools/tune_gemms.py --fresh --skip 128256 --out gpurun_out/t.csv
+(--fresh: re-tune every recorded shape, --skip: keep the committed winner of shapes matching the regex; the output
+is the committed file with the re-tuned rows replaced.)
 """
 import argparse
 import os
@@ -22,6 +26,9 @@ def main():
     ap.add_argument("--model", default="llama3_8b")
     ap.add_argument("--seq", type=int, default=8192)
     ap.add_argument("--mbs", type=int, default=1)
+    ap.add_argument("--out", default="", help="write the merged winners here instead of the committed file")
+    ap.add_argument("--fresh", action="store_true", help="re-tune shapes that already have a committed winner")
+    ap.add_argument("--skip", default="", help="regex: recorded GEMMs to leave alone (e.g. the LM head, 128256)")
     a = ap.parse_args()
 
     import torch
@@ -31,7 +38,10 @@ def main():
     from kubeoperator_amd.train import SyntheticTokens, TrainConfig, Trainer
     from kubeoperator_amd.train.gemm_tuning import results_path
 
-    out = results_path()
+    import re
+
+    committed = results_path()
+    out = os.path.abspath(a.out) if a.out else committed
     os.makedirs(os.path.dirname(out), exist_ok=True)
     untuned = os.path.join(os.path.dirname(out), "untuned_gemms.csv")
     for p in (untuned,):
@@ -41,9 +51,10 @@ def main():
     tun.enable(True)
     tun.tuning_enable(False)
     tun.record_untuned_enable(True)
-    tun.set_filename(out, insert_device_ordinal=False)
-    if os.path.exists(out):
-        tun.read_file(out)  # keep the committed winners: only shapes without one are recorded and tuned
+    # TunableOp's own exit-time dump goes to a scratch file; the merged winners are written below
+    tun.set_filename(out + ".tunableop", insert_device_ordinal=False)
+    if os.path.exists(committed) and not a.fresh:
+        tun.read_file(committed)  # keep the committed winners: only shapes without one are recorded and tuned
 
     info = init_distributed("auto")
     tr = Trainer(TrainConfig(model=a.model, micro_batch=a.mbs, seq_len=a.seq, warmup_steps=10, total_steps=100), info)
@@ -62,6 +73,8 @@ def main():
         return 1
     lines = [ln for ln in open(cands[0]) if ln.startswith(("Gemm", "ScaledGemm"))]
     lines = sorted(set(lines), key=lines.index)
+    if a.skip:
+        lines = [ln for ln in lines if not re.search(a.skip, ln)]
     print(f"{len(lines)} distinct GEMMs to tune", flush=True)
 
     tun.tuning_enable(True)
@@ -73,9 +86,25 @@ def main():
         tun._process_single_offline_gemm(ln, dev)
         torch.cuda.synchronize()
         print(f"[{i + 1}/{len(lines)}] {time.time() - t0:6.1f}s {ln.strip()[:160]}", flush=True)
-    # TunableOp writes every tuned result to the results file when the process exits
     res = tun.get_results()
-    print(f"wrote {len(res)} tuned results to {out}", flush=True)
+    new = {(r[0], r[1]): r for r in res}
+    rows, seen = [], set()
+    if os.path.exists(committed):
+        for ln in open(committed):
+            f = ln.rstrip("\n").split(",")
+            key = (f[0], f[1]) if len(f) >= 4 else None
+            if key in new:
+                r = new[key]
+                rows.append(f"{r[0]},{r[1]},{r[2]},{r[3]}\n")
+                seen.add(key)
+            else:
+                rows.append(ln if ln.endswith("\n") else ln + "\n")
+    for key, r in new.items():
+        if key not in seen:
+            rows.append(f"{r[0]},{r[1]},{r[2]},{r[3]}\n")
+    with open(out, "w") as fh:
+        fh.writelines(rows)
+    print(f"wrote {len(new)} tuned results merged into {out}", flush=True)
     for r in res:
         print("  ", r, flush=True)
     return 0

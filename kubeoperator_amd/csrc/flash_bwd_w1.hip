@@ -676,6 +676,17 @@ static int dkdv64_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, cons
     else KOP_LAUNCH_FWD(false, true, 0, false);
   }
   if (Hq == Hkv) {
+    if (diag != 0 && blk_layout && !qm) {  // timing ablations of the KT build (wrong results except 0)
+      switch (diag) {
+        case 1: KOP_LAUNCH(true, false, 1, true);
+        case 2: KOP_LAUNCH(true, false, 2, true);
+        case 4: KOP_LAUNCH(true, false, 4, true);
+        case 8: KOP_LAUNCH(true, false, 8, true);
+        case 12: KOP_LAUNCH(true, false, 12, true);
+        case 3: KOP_LAUNCH(true, false, 3, true);
+        default: break;
+      }
+    }
     if (blk_layout && !qm) KOP_LAUNCH(true, false, 0, true);  // KT tiles
     if (blk_layout) KOP_LAUNCH(true, true, 0, true);
     else KOP_LAUNCH(true, true, 0, false);

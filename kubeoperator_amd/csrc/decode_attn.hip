@@ -7,12 +7,12 @@
 //   o      [B, Hq * D]           bf16
 //
 // Memory-bound: every step streams the whole live cache (Llama-3-8B, 8k context: 4 MiB of K+V per sequence
-// and layer), so the kernel is built around coalesced 16-byte loads and reuse of each K/V row by all
-// G = Hq / Hkv query heads of its group, not around matrix cores (M = G <= 8 query rows per key tile would
-// leave MFMA 32-row tiles mostly empty).
+// and layer), so the kernels are built around coalesced 16-byte loads and reuse of each K/V row by all
+// G = Hq / Hkv query heads of its group.
 //
-// Pass 1: grid (splits, B * Hkv), 256 threads. A workgroup owns CH = 128 keys (KOP_DECODE_CH=256: 256) of one
-// (sequence, KV head).
+// Pass 1: grid (splits, B * Hkv), 256 threads. A workgroup owns CH = 128 keys of one (sequence, KV head).
+// Default: decode_attn_mfma_kernel (both products on 16x16x32 MFMAs, G heads as padded columns; below). The VALU
+// form (KOP_DECODE_ATTN=valu; KOP_DECODE_CH=256: 256 keys per workgroup):
 //   thread t = (key group kg = t / 16, segment sg = t % 16): the 16 threads of a key group read one 256-byte
 //   K row (D = 128) as 16 x 16 B -- a wave loads 4 whole rows per instruction -- and each keeps G partial dot
 //   products of its 8 dims, summed over the 16 lanes with 4 butterfly shuffles. Scores (already scaled by
@@ -21,8 +21,9 @@
 //   issued up front); the key groups' [G x D] partial sums are added with butterflies inside each wave, then
 //   over the 4 waves in LDS. Output per split: unnormalised acc [G, D], running max m and sum l (fp32).
 // Pass 2: grid B * Hq, D / 2 threads: o = sum_s acc_s 2^(m_s - M) / sum_s l_s 2^(m_s - M).
-#include "common.h"
+#include "attn_common.h"
 #include <cstdlib>
+#include <string>
 #include "kernels.h"
 
 namespace kop {
@@ -196,6 +197,192 @@ __global__ void __launch_bounds__(kThreads) decode_attn_split_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// Pass 1 on the matrix cores (default; KOP_DECODE_ATTN=valu selects the kernel above). The VALU form spends
+// its time on the per-key 16-lane butterflies of the scores and on the P . V FMAs, not on HBM: 3.9 TB/s at
+// batch 64 x 2k context (profiles/r5_experiments.md). Here each of the 4 waves owns 32 of the workgroup's 128
+// keys and both products are v_mfma_f32_16x16x32_bf16 with the G query heads as 16 padded columns:
+//   * S^T [16 keys x 16 heads] = K . Q^T: the A operand (lane l: key row, 8 dims) is one 16-byte load straight
+//     from the cache row; the 16 key rows of block b are keys 8(i >> 2) + 4b + (i & 3), so that lane l ends up
+//     holding its head (l & 15)'s scores of keys 8(l >> 4) .. +7 -- exactly the B operand P^T of the P . V
+//     product, with no lane exchange;
+//   * O^T [16 dims x 16 heads] += V^T . P^T: V^T comes from an LDS image of the wave's 32 V rows (LDS-DMA,
+//     lane-linear, each lane's source chunk XOR-permuted by the row so the ds_read_b64_tr_b16 transposed reads
+//     of a 32-lane half hit 64 distinct banks);
+//   * the softmax over the wave's 32 keys is lane-local plus two shuffles; the 4 waves' (m, l, O) meet in LDS
+//     once, and the split's partial goes out in the VALU kernel's format (same pass 2).
+// ---------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+template <int OFF>
+__device__ __forceinline__ bf16x4 dec_tr_read(uint32_t base) {
+  bf16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(base), "n"(OFF));
+  return r;
+}
+// XOR of a V row's 16-byte chunk slots in the LDS image (row r = 8g + 4h + q of the wave's 32 keys): spreads the
+// 8 rows a 32-lane half reads per transposed read over distinct chunk slots
+template <int ROWB>
+__device__ __forceinline__ int dec_vx(int r) {
+  if constexpr (ROWB == 256) return ((r & 3) << 1) | (((r >> 3) & 1) << 3);
+  else return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2);
+}
+
+template <int D, int G>
+__global__ void __launch_bounds__(kThreads) decode_attn_mfma_kernel(
+    const bf16_t* __restrict__ q, int64_t qs, const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc,
+    const int* __restrict__ lens, int Smax, int Hkv, float scale_log2, float* __restrict__ part_o,
+    float* __restrict__ part_ml, int nsplit) {
+  static_assert(D == 64 || D == 128, "head dim");
+  static_assert(G >= 1 && G <= 8, "heads per KV group");
+  constexpr int CH = 128, KW = 32, ROWB = D * 2, NS = D / 32, NC = D / 16, VPW = KW * ROWB / 1024;
+  constexpr int NWV = kThreads / 64;
+  // V images of the 4 waves (KW rows each); after the products the same bytes hold the waves' O^T partials
+  __shared__ __attribute__((aligned(16))) char s_v[NWV * KW * ROWB];
+  __shared__ float s_ml[NWV][G][2];
+  static_assert(NWV * G * D * 4 <= NWV * KW * ROWB, "partials fit the V images");
+  const int split = blockIdx.x;
+  const int b = blockIdx.y / Hkv, kvh = blockIdx.y % Hkv;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int len = min(lens[b], Smax);
+  const int k0 = split * CH;
+  float* po = part_o + (((int64_t)b * Hkv + kvh) * G * nsplit) * D;
+  float* pml = part_ml + (((int64_t)b * Hkv + kvh) * G * nsplit) * 2;
+  if (k0 >= len) {  // split past the sequence: an empty partial
+    if (t < G) {
+      pml[(t * nsplit + split) * 2] = kNegBig;
+      pml[(t * nsplit + split) * 2 + 1] = 0.f;
+    }
+    for (int i = t; i < G * D; i += kThreads) po[((i / D) * nsplit + split) * D + i % D] = 0.f;
+    return;
+  }
+  const int kb = k0 + KW * wv;  // the wave's first key
+  const bool live = kb < len;   // wave-uniform
+  const int col = lane & 15, g = lane >> 4;
+  const bf16_t* kbase = kc + ((int64_t)b * Hkv + kvh) * Smax * D;
+  const bf16_t* vbase = vc + ((int64_t)b * Hkv + kvh) * Smax * D;
+  char* const vimg = s_v + wv * (KW * ROWB);
+  float m = kNegBig, l = 0.f;
+  f32x4 acc[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (live) {
+    // Q^T B operand: head `col` (zero past G), dims 32s + 8g .. +7
+    bf16x8 qf[NS];
+    const bf16_t* qrow = q + (int64_t)b * qs + (int64_t)(kvh * G + (col < G ? col : 0)) * D + 8 * g;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      qf[s] = *reinterpret_cast<const bf16x8*>(qrow + 32 * s);
+      if (col >= G) qf[s] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+    // K A operand of block bb: key row kb + 8(col >> 2) + 4bb + (col & 3) (clamped: masked below), dims 32s + 8g
+    bf16x8 kf[2][NS];
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb) {
+      const int key = min(kb + 8 * (col >> 2) + 4 * bb + (col & 3), len - 1);
+      const bf16_t* kr = kbase + (int64_t)key * D + 8 * g;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) kf[bb][s] = *reinterpret_cast<const bf16x8*>(kr + 32 * s);
+    }
+    // V rows -> LDS image: piece i covers rows RPP i .. (1 KiB); lane -> (row, chunk slot), source chunk = slot ^ x
+    {
+      constexpr int SLOTS = ROWB / 16, RPP = 1024 / ROWB;
+#pragma unroll
+      for (int i = 0; i < VPW; ++i) {
+        const int r = RPP * i + lane / SLOTS, slot = lane % SLOTS;
+        const int key = min(kb + r, len - 1);
+        glds16(vbase + (int64_t)key * D + 8 * (slot ^ dec_vx<ROWB>(r)), vimg + 1024 * i);
+      }
+    }
+    // S^T: lane holds head `col`, keys kb + 8g + 4bb + j in sc[bb][j]
+    f32x4 sc[2];
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb) {
+      sc[bb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NS; ++s) sc[bb] = mfma16(kf[bb][s], qf[s], sc[bb]);
+    }
+    float p[8];
+    float mx = kNegBig;
+#pragma unroll
+    for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = kb + 8 * g + 4 * bb + j;
+        p[4 * bb + j] = key < len ? sc[bb][j] * scale_log2 : kNegBig;
+        mx = fmaxf(mx, p[4 * bb + j]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    m = mx;  // key kb is valid, so m is finite
+    float ls = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      p[j] = exp2f(p[j] - m);
+      ls += p[j];
+    }
+    ls += __shfl_xor(ls, 16, 64);
+    ls += __shfl_xor(ls, 32, 64);
+    l = ls;
+    const u32x4 pw = {pack2(p[0], p[1]), pack2(p[2], p[3]), pack2(p[4], p[5]), pack2(p[6], p[7])};
+    const bf16x8 pf = __builtin_bit_cast(bf16x8, pw);
+    // V^T A operand of dim block c: two transposed reads (rows 8g + 4h + q, chunk 2c + (p >> 1) of the image)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int tq = (lane >> 2) & 3, tp = lane & 3;
+    const int x = dec_vx<ROWB>(8 * g + tq) >> 1;  // the same for h = 0 / 1
+    const uint32_t vb = lds_addr(vimg) + (8 * g + tq) * ROWB + 8 * (tp & 1);
+#pragma unroll
+    for (int c0 = 0; c0 < NC; c0 += 4) {
+      bf16x4 tr[8];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t a = vb + 16 * ((2 * (c0 + c) + (tp >> 1)) ^ (2 * x));
+        tr[2 * c] = dec_tr_read<0>(a);
+        tr[2 * c + 1] = dec_tr_read<4 * ROWB>(a);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(tr[0]), "+v"(tr[1]), "+v"(tr[2]), "+v"(tr[3]), "+v"(tr[4]), "+v"(tr[5]), "+v"(tr[6]),
+                     "+v"(tr[7]));
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c0 + c] = mfma16(cat44(tr[2 * c], tr[2 * c + 1]), pf, acc[c0 + c]);
+    }
+  }
+  // ---- the 4 waves' (m, l, O^T) -> one partial of the split
+  __syncthreads();  // every wave is done with its V image
+  float* so = reinterpret_cast<float*>(s_v);  // [wave][head][D]
+  if (col < G) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) so[(wv * G + col) * D + 16 * c + 4 * g + r] = acc[c][r];
+    if (g == 0) {
+      s_ml[wv][col][0] = m;
+      s_ml[wv][col][1] = l;
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < G * D; i += kThreads) {
+    const int h = i / D, d = i % D;
+    float M = kNegBig;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) M = fmaxf(M, s_ml[w][h][0]);
+    float o = 0.f, L = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) {
+      const float wt = s_ml[w][h][1] > 0.f ? exp2f(s_ml[w][h][0] - M) : 0.f;
+      o += so[(w * G + h) * D + d] * wt;
+      L += s_ml[w][h][1] * wt;
+    }
+    po[((int64_t)h * nsplit + split) * D + d] = o;
+    if (d == 0) {
+      pml[(h * nsplit + split) * 2] = M;
+      pml[(h * nsplit + split) * 2 + 1] = L;
+    }
+  }
+}
+
 template <int D>
 __global__ void __launch_bounds__(D / 2) decode_attn_combine_kernel(const float* __restrict__ part_o,
                                                                     const float* __restrict__ part_ml, int Hq,
@@ -292,10 +479,27 @@ int decode_rope_append(bf16_t* qkv, int64_t qs, const float* cos_t, const float*
 
 int decode_attn_splits(int max_len) { return (max_len + chunk_keys() - 1) / chunk_keys(); }
 
+static int g_decode_mfma = -1;  // -1: read KOP_DECODE_ATTN (mfma, the default, | valu) on first use
+static bool decode_mfma() {
+  if (g_decode_mfma < 0) {
+    const char* e = getenv("KOP_DECODE_ATTN");
+    g_decode_mfma = (e && std::string(e) == "valu") ? 0 : 1;
+  }
+  return g_decode_mfma != 0;
+}
+int decode_attn_set_mfma(int on) {
+  const int old = decode_mfma() ? 1 : 0;
+  if (on >= 0) g_decode_mfma = on ? 1 : 0;
+  return old;
+}
+
 template <int D, int G>
 static void launch_split(const bf16_t* q, int64_t qs, const bf16_t* kc, const bf16_t* vc, const int* lens, int B,
                          int Smax, int Hkv, float sl2, float* po, float* pml, int nsplit, hipStream_t stream) {
-  if (chunk_keys() == 128)
+  if (chunk_keys() == 128 && decode_mfma())
+    decode_attn_mfma_kernel<D, G><<<dim3(nsplit, B * Hkv), kThreads, 0, stream>>>(q, qs, kc, vc, lens, Smax, Hkv, sl2,
+                                                                                 po, pml, nsplit);
+  else if (chunk_keys() == 128)
     decode_attn_split_kernel<D, G, 128><<<dim3(nsplit, B * Hkv), kThreads, 0, stream>>>(q, qs, kc, vc, lens, Smax, Hkv,
                                                                                        sl2, po, pml, nsplit);
   else

@@ -104,6 +104,7 @@ int embedding_bwd(const int* sorted_ids, const int64_t* perm, const bf16_t* dy, 
                   int64_t ldo, int T, int H, bool accumulate, hipStream_t stream);
 // decode_attn.hip: one query token per sequence against a [B, Hkv, Smax, D] KV cache (lens[b] valid keys),
 // split-K over 256-key chunks; part_o: B * Hq * nsplit * D floats, part_ml: B * Hq * nsplit * 2 floats
+int decode_attn_set_mfma(int on);  // 1: MFMA pass 1 (default), 0: VALU form; < 0: query only
 int decode_attn_splits(int max_len);
 // gemv.hip: y[M, N] = x[M, K] . W[N, K]^T for M <= 8 decode rows (K a multiple of 1024); 1 = unsupported shape
 int gemv_bf16(const bf16_t* x, const bf16_t* w, bf16_t* y, int M, int N, int K, int64_t xs, int64_t ws, int64_t ys,

@@ -47,20 +47,33 @@ def test_generate_cpu_decode_matches_fresh_prefill():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (128, 8, 8), (64, 16, 2), (128, 16, 2)])
-def test_decode_attention_kernel_matches_reference(D, Hq, Hkv):
+@pytest.mark.parametrize("impl", ["mfma", "valu"])
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (128, 8, 8), (64, 16, 2), (128, 16, 2), (64, 64, 8), (128, 64, 8)])
+def test_decode_attention_kernel_matches_reference(D, Hq, Hkv, impl):
+    """Both pass-1 kernels (csrc/decode_attn.hip) against the fp32 reference: lengths that end inside a wave's 32
+    keys, on a 128-key split boundary and one past it; cache rows past each length hold NaN, which no valid
+    output may pick up (masked keys of a partial tile read a clamped valid row instead)."""
     from kubeoperator_amd.ops import functional as kf
+    from kubeoperator_amd.ops import load
 
     torch.manual_seed(0)
-    B, Smax = 5, 1300
-    lens = torch.tensor([1, 255, 256, 700, 1300], dtype=torch.int32, device="cuda")
+    B, Smax = 6, 1300
+    lens = torch.tensor([1, 33, 255, 256, 700, 1300], dtype=torch.int32, device="cuda")
     kc = torch.randn(B, Hkv, Smax, D, device="cuda").to(torch.bfloat16)
     vc = torch.randn(B, Hkv, Smax, D, device="cuda").to(torch.bfloat16)
+    for i, n in enumerate(lens.tolist()):
+        kc[i, :, n:] = float("nan")
+        vc[i, :, n:] = float("nan")
     qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda").to(torch.bfloat16)
     q = qkv[:, : Hq * D]  # strided row view, as the generator passes it
     scale = 1.0 / math.sqrt(D)
-    got = kf.decode_attention(q, kc, vc, lens, int(lens.max()), scale)
+    old = load().decode_attn_set_mfma(1 if impl == "mfma" else 0)
+    try:
+        got = kf.decode_attention(q, kc, vc, lens, int(lens.max()), scale)
+    finally:
+        load().decode_attn_set_mfma(old)
     want = ref.decode_attention_ref(q, kc, vc, lens, scale)
+    assert torch.isfinite(got.float()).all()
     err = ((got.float() - want.float()).abs().max() / want.float().abs().max()).item()
     assert err < 2e-2, err
 

@@ -47,6 +47,7 @@ def main():
     for B, graph, f8 in runs:
         gen = LlamaGenerator(m, max_batch=B, max_seq=a.prompt + a.steps + 3, graph=bool(graph), fp8=bool(f8))
         ids = torch.randint(0, cfg.vocab_size, (B, a.prompt), device="cuda")
+        gen.prefill(ids)  # untimed: first-call library / workspace setup (the timed prefill rewrites the same rows)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         logits = gen.prefill(ids)

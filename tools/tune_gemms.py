@@ -14,11 +14,32 @@ is the committed file with the re-tuned rows replaced.)
 """
 import argparse
 import os
+import re
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+
+def merge_results(committed_lines, results):
+    """The committed TunableOp file with the rows of re-tuned signatures replaced (Validator and untouched rows kept
+    in place) and signatures new to it appended. ``results``: tuples (op, params, solution, ms)."""
+    new = {(r[0], r[1]): r for r in results}
+    rows, seen = [], set()
+    for ln in committed_lines:
+        f = ln.rstrip("\n").split(",")
+        key = (f[0], f[1]) if len(f) >= 4 and not f[0].startswith("Validator") else None
+        if key in new:
+            r = new[key]
+            rows.append(f"{r[0]},{r[1]},{r[2]},{r[3]}\n")
+            seen.add(key)
+        else:
+            rows.append(ln if ln.endswith("\n") else ln + "\n")
+    for key, r in new.items():
+        if key not in seen:
+            rows.append(f"{r[0]},{r[1]},{r[2]},{r[3]}\n")
+    return rows
 
 
 def main():
@@ -37,8 +58,6 @@ def main():
     from kubeoperator_amd.parallel.dist import init_distributed
     from kubeoperator_amd.train import SyntheticTokens, TrainConfig, Trainer
     from kubeoperator_amd.train.gemm_tuning import results_path
-
-    import re
 
     committed = results_path()
     out = os.path.abspath(a.out) if a.out else committed
@@ -87,21 +106,8 @@ def main():
         torch.cuda.synchronize()
         print(f"[{i + 1}/{len(lines)}] {time.time() - t0:6.1f}s {ln.strip()[:160]}", flush=True)
     res = tun.get_results()
-    new = {(r[0], r[1]): r for r in res}
-    rows, seen = [], set()
-    if os.path.exists(committed):
-        for ln in open(committed):
-            f = ln.rstrip("\n").split(",")
-            key = (f[0], f[1]) if len(f) >= 4 else None
-            if key in new:
-                r = new[key]
-                rows.append(f"{r[0]},{r[1]},{r[2]},{r[3]}\n")
-                seen.add(key)
-            else:
-                rows.append(ln if ln.endswith("\n") else ln + "\n")
-    for key, r in new.items():
-        if key not in seen:
-            rows.append(f"{r[0]},{r[1]},{r[2]},{r[3]}\n")
+    rows = merge_results(open(committed).readlines() if os.path.exists(committed) else [], res)
+    new = {(r[0], r[1]) for r in res}
     with open(out, "w") as fh:
         fh.writelines(rows)
     print(f"wrote {len(new)} tuned results merged into {out}", flush=True)

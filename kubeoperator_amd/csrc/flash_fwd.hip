@@ -517,15 +517,19 @@ int flash_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o,
   if (qs % 8 || ks % 8 || vs % 8 || os % 8) return -2;
   const float sl2 = scale * 1.4426950408889634f;
   // KOP_FWD_VARIANT: 8 lockstep 8-wave kernel (scalar-FMA softmax), 10 the same with packed FMAs, 9 staggered halves,
-  // < 8 the 4-wave kernel. Defaults per head dim from same-box probes (profiles/r3_fwd_variant_probe.jsonl): D = 128 ->
-  // 8 (2-3 % over 10: packed f32 VALU beside MFMAs is an anti-lever, MI355X_MICROARCH.md); D = 64 causal -> 4-wave
-  // (short causal sweeps, more workgroups per CU), non-causal -> 8.
+  // 16 the 8-wave structure on 16x16x32 MFMAs, < 8 the 4-wave kernel. Defaults per head dim from same-box probes:
+  // D = 128 -> 8 (2-3 % over 10, profiles/r3_fwd_variant_probe.jsonl; 3-4 % over 16, whose 16-cycle MFMAs hold
+  // the VALU issue half the time instead of a quarter, profiles/r5_fwd16_vdepth_ab.jsonl); D = 64 -> 16 (7 % over the
+  // 4-wave kernel causal, 11 % over 8 non-causal at the GPT-2 shape; S % 256 == 0, else the 4-wave kernel).
   const int env_variant = flash_attn_set_fwd_variant(-3);  // current setting (-3 changes nothing)
-  int variant = env_variant >= 0 ? env_variant : (D == 64 && causal) ? 0 : 8;
-  if (ot != nullptr && variant < 8) variant = 8;  // O^T comes only from the 8-wave kernel
+  int variant = env_variant >= 0 ? env_variant : (D == 64) ? 16 : 8;
+  if (ot != nullptr && variant < 8) variant = 8;  // O^T comes only from the 8-wave kernels
   // 12: the 4-wave one-wave-per-SIMD kernel, 64 rows per wave, hand-scheduled double pipeline (csrc/flash_fwd4.hip;
   // D = 128). An 8-wave double pipeline (QK of tile t+1 beside the softmax of tile t, 2 waves per SIMD) ran 15 %
   // slower and spilled: profiles/r5_experiments.md
+  // 16: the 8-wave structure on 16x16x32 MFMAs (csrc/flash_fwd16.hip)
+  if (S % 256 == 0 && variant == 16 && (D == 64 || D == 128))
+    return flash_attn_fwd16(q, k, v, o, lse, B, S, Hq, Hkv, D, qs, ks, vs, os, sl2, causal, stream, ot);
   if (S % 256 == 0 && variant == 12 && D == 128) {
     return flash_attn_fwd4x64(q, k, v, o, lse, B, S, Hq, Hkv, D, qs, ks, vs, os, sl2, causal, stream, ot);
   }

@@ -71,6 +71,10 @@ int flash_attn_fwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o,
                    int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, float scale, bool causal,
                    hipStream_t stream, bf16_t* ot = nullptr);
 // 4-wave one-wave-per-SIMD forward (csrc/flash_fwd4.hip); sl2 = scale * log2(e); S % 256 == 0, D 64 / 128
+// flash_fwd16.hip: the 8-wave forward on 16x16x32 MFMAs (KOP_FWD_VARIANT=16; D 64 / 128, S % 256 == 0)
+int flash_attn_fwd16(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int S, int Hq,
+                     int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, float sl2, bool causal,
+                     hipStream_t stream, bf16_t* ot);
 int flash_attn_fwd4x64(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* o, float* lse, int B, int S, int Hq,
                        int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, float sl2, bool causal,
                        hipStream_t stream, bf16_t* ot);

@@ -795,7 +795,7 @@ def rope_attention(qkv, cos, sin, B, S, Hq, Hkv, D, causal=True, scale=None, use
         a, c = Hq * D, (Hq + Hkv) * D
         o, _ = _attn_ref_autograd(x[:, :a], x[:, a:c], x[:, c:], B, S, Hq, Hkv, D, causal, scale)
         return (o, None) if want_ot else o
-    ot = bool(want_ot) and S % 256 == 0 and D in (64, 128) and os.environ.get("KOP_FWD_VARIANT", "10") in ("8", "9", "10", "12")
+    ot = bool(want_ot) and S % 256 == 0 and D in (64, 128) and os.environ.get("KOP_FWD_VARIANT", "10") in ("8", "9", "10", "12", "16")
     out = _RopeAttention.apply(qkv, cos, sin, B, S, Hq, Hkv, D, causal, scale, use_rope, inplace, box, ot)
     if want_ot and not ot:
         return out, None

@@ -214,10 +214,10 @@ def test_flash_attention_fwd(D, causal):
     check_against_bf16("o", o.reshape(-1, D), o_ref.reshape(-1, D), ob.reshape(-1, D))
 
 
-@pytest.mark.parametrize("variant", [-1, 10, 8, 9, 0])
+@pytest.mark.parametrize("variant", [-1, 10, 8, 9, 0, 16])
 def test_flash_attention_fwd_spiked_rescale(variant):
     """force the online-softmax rescale branch: a large score late in the key sweep (every forward kernel:
-    -1 the default, 8 / 9 / 10 the 8-wave kernel, 0 the 4-wave kernel)."""
+    -1 the default, 8 / 9 / 10 the 8-wave kernel, 0 the 4-wave kernel, 16 the 16x16x32-MFMA kernel)."""
     from kubeoperator_amd.ops.functional import flash_attention
     from kubeoperator_amd.ops.reference import attention_ref
 
@@ -236,17 +236,16 @@ def test_flash_attention_fwd_spiked_rescale(variant):
         lib().flash_attn_set_fwd_variant(old)
 
 
-@pytest.mark.parametrize("variant", [8, 10])
+@pytest.mark.parametrize("variant,D", [(8, 128), (10, 128), (16, 128), (16, 64)])
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 512, 8, 2), (1, 1024, 4, 4), (2, 256, 6, 3)])
 @pytest.mark.parametrize("causal", [True, False])
-def test_flash_attention_fwd_variants_d128(variant, B, S, Hq, Hkv, causal):
-    """the 8-wave forward (scalar / packed FMA softmax) against the fp32 reference at D = 128 and GQA groups of 4, 1
-    and 2, with and without the O^T output (which must be the exact transpose of O)."""
+def test_flash_attention_fwd_variants_d128(variant, D, B, S, Hq, Hkv, causal):
+    """the 8-wave forward (scalar / packed FMA softmax; 16: on 16x16x32 MFMAs, also at D = 64) against the fp32
+    reference with GQA groups of 4, 1 and 2, with and without the O^T output (which must be the exact transpose of O)."""
     from kubeoperator_amd.ops.reference import attention_ref
 
     old = lib().flash_attn_set_fwd_variant(variant)
     try:
-        D = 128
         torch.manual_seed(B * S + Hq)
         qkv = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
         a, c = Hq * D, (Hq + Hkv) * D

@@ -90,7 +90,7 @@ def test_flash_forward_writes_o_transpose(D):
     o0 = torch.empty(T, Hq * D, device="cuda", dtype=torch.bfloat16)
     o1, ot = torch.empty_like(o0), torch.empty(Hq * D, T, device="cuda", dtype=torch.bfloat16)
     l0, l1 = (torch.empty(B * Hq * S, device="cuda") for _ in range(2))
-    old = _lib().flash_attn_set_fwd_variant(8)  # the plain call on the same 8-wave kernel (causal D 64 defaults to 4 waves)
+    old = _lib().flash_attn_set_fwd_variant(8)  # both calls on the same kernel (pinned: the default depends on D)
     try:
         _lib().flash_attn_fwd(q, k, v, o0, l0, B, S, Hq, Hkv, D, D ** -0.5, True)
         _lib().flash_attn_fwd_t(q, k, v, o1, ot, l1, B, S, Hq, Hkv, D, D ** -0.5, True)

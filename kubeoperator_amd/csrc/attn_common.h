@@ -79,6 +79,25 @@ __device__ __forceinline__ float max3f(float a, float b, float c) {
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
   return d;
 }
+// max / sum over lanes l and l ^ 16 (16-lane rows 0 <-> 1, 2 <-> 3) and l ^ 32 (halves) with v_permlane16/32_swap:
+// a register exchange, where __shfl_xor is a ds_bpermute round trip through the LDS pipe (on a softmax's critical
+// path: profiles/r5_experiments.md, the 16x16x32 forward)
+__device__ __forceinline__ float xor16_max(float x) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+}
+__device__ __forceinline__ float xor32_max(float x) {
+  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+}
+__device__ __forceinline__ float xor16_sum(float x) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+}
+__device__ __forceinline__ float xor32_sum(float x) {
+  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+}
 // max over the 32 scores of two accumulators: 16 v_max3
 __device__ __forceinline__ float max32(const f32x16& a, const f32x16& b) {
   float m = max3f(a[0], b[0], a[1]);

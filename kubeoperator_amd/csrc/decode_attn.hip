@@ -314,8 +314,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_mfma_kernel(
         p[4 * bb + j] = key < len ? sc[bb][j] * scale_log2 : kNegBig;
         mx = fmaxf(mx, p[4 * bb + j]);
       }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = xor32_max(xor16_max(mx));
     m = mx;  // key kb is valid, so m is finite
     float ls = 0.f;
 #pragma unroll
@@ -323,8 +322,7 @@ __global__ void __launch_bounds__(kThreads) decode_attn_mfma_kernel(
       p[j] = exp2f(p[j] - m);
       ls += p[j];
     }
-    ls += __shfl_xor(ls, 16, 64);
-    ls += __shfl_xor(ls, 32, 64);
+    ls = xor32_sum(xor16_sum(ls));
     l = ls;
     const u32x4 pw = {pack2(p[0], p[1]), pack2(p[2], p[3]), pack2(p[4], p[5]), pack2(p[6], p[7])};
     const bf16x8 pf = __builtin_bit_cast(bf16x8, pw);

@@ -134,7 +134,7 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_fwd_kernel(const bf16_t* __rest
       float mx = fmaxf(s0[0], s1[0]);
 #pragma unroll
       for (int j = 1; j < 16; ++j) mx = fmaxf(mx, fmaxf(s0[j], s1[j]));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = xor32_max(mx);
       const float mt = mx * scale_log2;
       if (__any(mt > m + 8.f)) {
         const float mnew = fmaxf(m, mt);
@@ -189,7 +189,7 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_fwd_kernel(const bf16_t* __rest
 #undef KBUF
 #undef VBUF
 
-  const float lt = l + __shfl_xor(l, 32, 64);
+  const float lt = xor32_sum(l);
   const float inv = 1.f / lt;
   if (hh == 0) lse[((int64_t)(b * Hq + hq)) * S + q0w + r] = (m + __log2f(lt)) * 0.69314718056f;
   bf16_t* op = o + (int64_t)(b * S + q0w + r) * os + hq * D;
@@ -349,7 +349,7 @@ __global__ void __launch_bounds__(512, 1) fa_fwd8_kernel(const bf16_t* __restric
     bf16x4 ta[NR], tb[DB ? NR : 1];
     vread(Vb, std::integral_constant<int, 0>{}, ta);  // flies under the softmax
     float mx = max32(s0, s1);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = xor32_max(mx);
     const float mt = mx * scale_log2;
     if (__any(mt > m + 8.f)) {
       const float mnew = fmaxf(m, mt);
@@ -430,7 +430,7 @@ __global__ void __launch_bounds__(512, 1) fa_fwd8_kernel(const bf16_t* __restric
 #undef KBUF
 #undef VBUF
 
-  const float lt = l + __shfl_xor(l, 32, 64);
+  const float lt = xor32_sum(l);
   const float inv = 1.f / lt;
   if (hh == 0) lse[((int64_t)(b * Hq + hq)) * S + q0w + r] = (m + __log2f(lt)) * 0.69314718056f;
   if (ot != nullptr) {

@@ -52,24 +52,6 @@ __device__ __forceinline__ void dma_img(char* lds, const bf16_t* src, int64_t rs
     glds16(src + (int64_t)row * rs + ch * 8, lds + piece * 1024);
   }
 }
-// max / sum over lanes l and l ^ 16 (rows 0 <-> 1, 2 <-> 3) and l ^ 32 (halves) with v_permlane16/32_swap: no LDS
-// round trip (a __shfl_xor here was a ds_bpermute on the softmax's critical path)
-__device__ __forceinline__ float swap16_max(float x) {
-  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
-}
-__device__ __forceinline__ float swap32_max(float x) {
-  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
-}
-__device__ __forceinline__ float swap16_sum(float x) {
-  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(p[0]) + __uint_as_float(p[1]);
-}
-__device__ __forceinline__ float swap32_sum(float x) {
-  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(p[0]) + __uint_as_float(p[1]);
-}
 template <int CNT>
 __device__ __forceinline__ void wait_k4(bf16x8* t) {
   asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]) : "n"(CNT));
@@ -201,7 +183,7 @@ __global__ void __launch_bounds__(512, 1) fa_fwd16_kernel(const bf16_t* __restri
       mx = max3f(mx, sc[qq][2][3], sc[qq][3][0]);
       mx = max3f(mx, sc[qq][3][1], sc[qq][3][2]);
       mx = fmaxf(mx, sc[qq][3][3]);
-      mt[qq] = swap32_max(swap16_max(mx)) * scale_log2;
+      mt[qq] = xor32_max(xor16_max(mx)) * scale_log2;
     }
     if (__any(mt[0] > m[0] + 8.f || mt[1] > m[1] + 8.f)) {
 #pragma unroll
@@ -276,7 +258,7 @@ __global__ void __launch_bounds__(512, 1) fa_fwd16_kernel(const bf16_t* __restri
   const int64_t T = (int64_t)B * S;
 #pragma unroll
   for (int qq = 0; qq < 2; ++qq) {
-    const float lt = swap32_sum(swap16_sum(l[qq]));
+    const float lt = xor32_sum(xor16_sum(l[qq]));
     const float inv = 1.f / lt;
     const int qi = q0w + 16 * qq + col;
     if (g == 0) lse[((int64_t)(b * Hq + hq)) * S + qi] = (m[qq] + __log2f(lt)) * 0.69314718056f;

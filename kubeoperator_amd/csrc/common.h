@@ -54,15 +54,34 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
   return v;
 }
 
+// Wave reductions without the LDS pipe: DPP inside each 16-lane row (lane ^ 1, ^ 2, then the mirrored quad and
+// half), v_permlane16_swap / v_permlane32_swap across rows. Every step adds a value to its partner's, so all 64
+// lanes end with the same total (a + b == b + a). (A __shfl_xor loop is six ds_bpermute round trips.)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float swap16_f32(float v, bool mx) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return mx ? fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1])) : __uint_as_float(p[0]) + __uint_as_float(p[1]);
+}
+__device__ __forceinline__ float swap32_f32(float v, bool mx) {
+  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return mx ? fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1])) : __uint_as_float(p[0]) + __uint_as_float(p[1]);
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_f32<0xB1>(v);   // quad_perm [1, 0, 3, 2]: lane ^ 1
+  v += dpp_f32<0x4E>(v);   // quad_perm [2, 3, 0, 1]: lane ^ 2
+  v += dpp_f32<0x141>(v);  // row_half_mirror: the other quad of the 8-lane half
+  v += dpp_f32<0x140>(v);  // row_mirror: the other half of the 16-lane row
+  return swap32_f32(swap16_f32(v, false), false);
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmaxf(v, dpp_f32<0xB1>(v));
+  v = fmaxf(v, dpp_f32<0x4E>(v));
+  v = fmaxf(v, dpp_f32<0x141>(v));
+  v = fmaxf(v, dpp_f32<0x140>(v));
+  return swap32_f32(swap16_f32(v, true), true);
 }
 
 // Block-wide sum for blocks of NW waves; `red` must hold NW floats of LDS.

@@ -52,10 +52,7 @@ __global__ void __launch_bounds__(256) gemv_bf16_kernel(const bf16_t* __restrict
   for (int m = 0; m < M; ++m)
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      float v = acc[m][r];
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-      acc[m][r] = v;
+      acc[m][r] = wave_sum(acc[m][r]);
     }
   if (lane == 0) {
 #pragma unroll

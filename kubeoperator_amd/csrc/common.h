@@ -76,6 +76,18 @@ __device__ __forceinline__ float wave_sum(float v) {
   v += dpp_f32<0x140>(v);  // row_mirror: the other half of the 16-lane row
   return swap32_f32(swap16_f32(v, false), false);
 }
+// sum over each aligned group of N lanes (N = 2 .. 64), every lane of a group ending with its total
+template <int N>
+__device__ __forceinline__ float group_sum(float v) {
+  static_assert(N == 2 || N == 4 || N == 8 || N == 16 || N == 32 || N == 64, "power-of-two group");
+  v += dpp_f32<0xB1>(v);
+  if constexpr (N >= 4) v += dpp_f32<0x4E>(v);
+  if constexpr (N >= 8) v += dpp_f32<0x141>(v);
+  if constexpr (N >= 16) v += dpp_f32<0x140>(v);
+  if constexpr (N >= 32) v = swap16_f32(v, false);
+  if constexpr (N >= 64) v = swap32_f32(v, false);
+  return v;
+}
 __device__ __forceinline__ float wave_max(float v) {
   v = fmaxf(v, dpp_f32<0xB1>(v));
   v = fmaxf(v, dpp_f32<0x4E>(v));

@@ -74,8 +74,7 @@ __global__ void __launch_bounds__(256) fa_bwd_delta_kernel(const bf16_t* __restr
 #pragma unroll
       for (int i = 0; i < 8; ++i) a += x[i] * y[i];
     }
-#pragma unroll
-    for (int off = LPR / 2; off > 0; off >>= 1) a += __shfl_xor(a, off, 64);
+    a = group_sum<LPR>(a);  // DPP inside the row's lane group (a __shfl_xor loop was ds_bpermute round trips)
     if (s < S && c == 0) {
       const int64_t i = (int64_t)bh * S + s;
       delta[i] = a;

@@ -125,11 +125,14 @@ def test_swiglu_fwd_bwd():
     assert rel_err(gu.grad, g.grad) < 2e-2
 
 
-def test_gelu_fwd_bwd():
+@pytest.mark.parametrize("rows", [64, 2051])
+def test_gelu_fwd_bwd(rows):
+    """64 rows: one chunk per thread; 2051 rows: more 16-byte chunks than the 2048 x 256-thread grid holds (the
+    grid-stride loop's second pass ends part-way through the grid)."""
     from kubeoperator_amd.ops.functional import gelu
 
     torch.manual_seed(4)
-    x = (3 * torch.randn(64, 3072, device=DEV)).to(torch.bfloat16).requires_grad_(True)
+    x = (3 * torch.randn(rows, 3072, device=DEV)).to(torch.bfloat16).requires_grad_(True)
     y = gelu(x)
     dy = torch.randn_like(y)
     (y.float() * dy.float()).sum().backward()

@@ -29,18 +29,20 @@ __global__ void __launch_bounds__(NT) ce_fwd_kernel(bf16_t* __restrict__ logits,
   bf16_t* x = logits + row * ld;
   const int V8 = VEC ? (V >> 3) : 0;
   float m = -INFINITY, s = 0.f;
+  // pass 1 in the log2 domain: max on the raw logits, exp2(fma(f, log2 e, -m log2 e)) -- one FMA + one v_exp_f32 per
+  // logit (the __expf form cost a subtract, a multiply and the exponential)
+  constexpr float L2E = 1.4426950408889634f;
   const u32x4* xv = reinterpret_cast<const u32x4*>(x);
   for (int c = threadIdx.x; c < V8; c += NT) {
     float f[8];
     unpack8(xv[c], f);
-    float cm = f[0];
-#pragma unroll
-    for (int i = 1; i < 8; ++i) cm = fmaxf(cm, f[i]);
+    const float cm = fmaxf(fmaxf(fmaxf(f[0], f[1]), fmaxf(f[2], f[3])), fmaxf(fmaxf(f[4], f[5]), fmaxf(f[6], f[7])));
     const float nm = fmaxf(m, cm);
+    const float nb = -nm * L2E;
     float add = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) add += __expf(f[i] - nm);
-    s = s * __expf(m - nm) + add;
+    for (int i = 0; i < 8; ++i) add += __builtin_amdgcn_exp2f(fmaf(f[i], L2E, nb));
+    s = s * __builtin_amdgcn_exp2f((m - nm) * L2E) + add;
     m = nm;
   }
   for (int i = V8 * 8 + threadIdx.x; i < V; i += NT) {
@@ -71,27 +73,30 @@ __global__ void __launch_bounds__(NT) ce_fwd_kernel(bf16_t* __restrict__ logits,
   const float lse = M + __logf(Ssum);
   const int64_t t = tgt[row];
   const bool valid = t != ignore_index;
+  const float xt = valid ? bf2f(x[t]) : 0.f;
   if (threadIdx.x == 0) {
     lse_rows[row] = lse;
-    loss_rows[row] = valid ? (lse - bf2f(x[t])) : 0.f;
+    loss_rows[row] = valid ? (lse - xt) : 0.f;
   }
   if (!write_grad) return;
   __syncthreads();  // everyone has read x[t] above before it is overwritten
   const float sc = valid ? scale_p[0] : 0.f;
+  // pass 2: (softmax - onehot) * scale = exp2(f log2 e - lse log2 e + log2 sc) for every logit (the scale folded into
+  // the exponent: one FMA + one exponential + the pack), then the target's own element is rewritten once below
+  // instead of an index compare per logit
+  const float b2 = sc > 0.f ? (__log2f(sc) - lse * L2E) : -INFINITY;
   u32x4* xw = reinterpret_cast<u32x4*>(x);
   for (int c = threadIdx.x; c < V8; c += NT) {
     float f[8];
     unpack8(xw[c], f);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float p = __expf(f[i] - lse);
-      f[i] = (p - ((int64_t)(c * 8 + i) == t ? 1.f : 0.f)) * sc;
-    }
+    for (int i = 0; i < 8; ++i) f[i] = __builtin_amdgcn_exp2f(fmaf(f[i], L2E, b2));
     xw[c] = pack8(f);
   }
-  for (int i = V8 * 8 + threadIdx.x; i < V; i += NT) {
-    const float p = __expf(bf2f(x[i]) - lse);
-    x[i] = f2bf((p - (i == t ? 1.f : 0.f)) * sc);
+  for (int i = V8 * 8 + threadIdx.x; i < V; i += NT) x[i] = f2bf(__builtin_amdgcn_exp2f(fmaf(bf2f(x[i]), L2E, b2)));
+  if (valid) {
+    __syncthreads();  // the target's element has been written by its owner above
+    if (threadIdx.x == 0) x[t] = f2bf((__expf(xt - lse) - 1.f) * sc);
   }
 }
 

@@ -143,8 +143,10 @@ def test_gelu_fwd_bwd(rows):
     assert rel_err(x.grad, xf.grad) < 2e-2
 
 
-@pytest.mark.parametrize("V", [128256, 50257, 1000])
+@pytest.mark.parametrize("V", [128256, 50304, 50257, 1000])
 def test_cross_entropy_lmhead(V):
+    """128256: the two-pass kernel; 50304 (GPT-2's padded vocabulary) and 1000: the register-resident rows;
+    50257: the scalar (unaligned) path; every seventh target ignored."""
     from kubeoperator_amd.ops.functional import cross_entropy_lmhead
 
     torch.manual_seed(5)

@@ -104,6 +104,40 @@ Tensor norm_bwd(const Tensor& dy, const Tensor& s, const Tensor& w, const Tensor
   return dx;
 }
 
+// the norm backward without its weight-gradient fold: [dx, fp32 partials]; norm_bwd_reduce_ folds the partials into
+// dw (and db for LayerNorm) -- on the weight-gradient stream, off the data-gradient chain (ops/functional.py)
+std::vector<Tensor> norm_bwd_parts(const Tensor& dy, const Tensor& s, const Tensor& w, const Tensor& rstd,
+                                   const c10::optional<Tensor>& mean, const c10::optional<Tensor>& dres,
+                                   bool layernorm) {
+  check_bf16(dy, "dy");
+  check_bf16(s, "s");
+  TORCH_CHECK(dy.is_contiguous() && s.is_contiguous(), "norm_bwd_parts inputs must be contiguous");
+  const int H = (int)s.size(-1);
+  const int rows = (int)(s.numel() / H);
+  auto dx = at::empty_like(s);
+  const int parts = kop::norm_bwd_partial_rows(rows, H);
+  auto part = at::empty({(layernorm ? 2 : 1) * (int64_t)parts, (int64_t)H}, s.options().dtype(at::kFloat));
+  rc(kop::norm_bwd(bp(dy), bp(s), bp(w), rstd.data_ptr<float>(),
+                   mean.has_value() && mean->defined() ? mean->data_ptr<float>() : nullptr, cbp(dres), bp(dx),
+                   part.data_ptr<float>(), nullptr, nullptr, rows, H, layernorm, 0, cur_stream()),
+     "norm_bwd_parts");
+  return {dx, part};
+}
+
+void norm_bwd_reduce_(const Tensor& part, const Tensor& dw, const c10::optional<Tensor>& db, bool layernorm,
+                      bool accumulate) {
+  check_f32(part, "part");
+  check_bf16(dw, "dw");
+  TORCH_CHECK(part.dim() == 2 && part.is_contiguous() && dw.is_contiguous() && part.size(1) == dw.numel(),
+              "norm_bwd_reduce_: part must be [k * parts, H] with H = dw.numel()");
+  TORCH_CHECK(!layernorm || (db.has_value() && db->defined() && db->numel() == dw.numel()), "LayerNorm needs db");
+  const int H = (int)part.size(1);
+  const int parts = (int)(part.size(0) / (layernorm ? 2 : 1));
+  rc(kop::norm_bwd_reduce(part.data_ptr<float>(), parts, H, bp(dw), layernorm ? bp(*db) : nullptr, layernorm,
+                          accumulate ? 1 : 0, cur_stream()),
+     "norm_bwd_reduce_");
+}
+
 // RMSNorm with the transposed companion: [y, s, rstd, y^T] (s undefined without a residual)
 std::vector<Tensor> rms_norm_fwd_t(const Tensor& x, const c10::optional<Tensor>& residual, const Tensor& w, double eps) {
   check_bf16(x, "x");
@@ -530,6 +564,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("ARCH") = "gfx950";
   m.def("norm_fwd", &norm_fwd);
   m.def("norm_bwd", &norm_bwd);
+  m.def("norm_bwd_parts", &norm_bwd_parts);
+  m.def("norm_bwd_reduce_", &norm_bwd_reduce_);
   m.def("rms_norm_fwd_t", &rms_norm_fwd_t);
   m.def("rms_norm_bwd_t", &rms_norm_bwd_t);
   m.def("bias_grad_", &bias_grad_);

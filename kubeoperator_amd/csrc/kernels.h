@@ -22,7 +22,9 @@ int rms_norm_bwd_t(const bf16_t* dy, const bf16_t* s, const bf16_t* w, const flo
                    hipStream_t stream);
 int norm_bwd(const bf16_t* dy, const bf16_t* s, const bf16_t* w, const float* rstd, const float* mean,
              const bf16_t* dres, bf16_t* dx, float* part, bf16_t* dw, bf16_t* db, int rows, int H, bool layernorm,
-             int accumulate, hipStream_t stream);
+             int accumulate, hipStream_t stream);  // dw == nullptr: fp32 partials only (norm_bwd_reduce folds them)
+int norm_bwd_reduce(const float* part, int parts, int H, bf16_t* dw, bf16_t* db, bool layernorm, int accumulate,
+                    hipStream_t stream);
 int bias_grad_parts(int rows, int H);
 int bias_grad(const bf16_t* dy, int rows, int H, float* part, bf16_t* db, int accumulate, hipStream_t stream);
 

@@ -541,9 +541,15 @@ int norm_bwd(const bf16_t* dy, const bf16_t* s, const bf16_t* w, const float* rs
   NORM_BWD_DISPATCH(3)
   NORM_BWD_DISPATCH(4)
   if (!done) return -2;
+  if (dw == nullptr) return 0;  // partials only: the caller folds them with norm_bwd_reduce (on the side stream)
+  return norm_bwd_reduce(part, grid, H, dw, db, layernorm, accumulate, stream);
+}
+
+int norm_bwd_reduce(const float* part, int parts, int H, bf16_t* dw, bf16_t* db, bool layernorm, int accumulate,
+                    hipStream_t stream) {
   const int cg = col_reduce_blocks(H);
-  col_reduce_kernel<<<cg, 1024, 0, stream>>>(part, grid, H, dw, accumulate);
-  if (layernorm) col_reduce_kernel<<<cg, 1024, 0, stream>>>(part + (size_t)grid * H, grid, H, db, accumulate);
+  col_reduce_kernel<<<cg, 1024, 0, stream>>>(part, parts, H, dw, accumulate);
+  if (layernorm) col_reduce_kernel<<<cg, 1024, 0, stream>>>(part + (size_t)parts * H, parts, H, db, accumulate);
   return 0;
 }
 

@@ -57,6 +57,31 @@ def _lib():
 SIDE_LAG_CYCLES = int(os.environ.get("KOP_SIDE_LAG_CYCLES", "0"))
 
 
+_NORM_SIDE = os.environ.get("KOP_NORM_SIDE", "1") != "0"  # norm weight-gradient folds on the side stream (A/B: 0)
+
+
+def _side_active(w) -> bool:
+    """The weight-gradient side stream takes launches for ``w`` (the flat store runs one, not under capture)."""
+    hooks = getattr(w, "_kop_hooks", None)
+    return (hooks is not None and hooks.store.wgrad_stream and w.is_cuda
+            and not torch.cuda.is_current_stream_capturing())
+
+
+def _side_launch(w, launch, *inputs) -> None:
+    """Run ``launch()`` on ``w``'s weight-gradient stream once it has caught up with the compute stream; ``inputs``
+    stay alive (and their memory unreused) until that stream has passed them."""
+    store = w._kop_hooks.store
+    side = store.side_stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        if SIDE_LAG_CYCLES > 0:
+            torch.cuda._sleep(SIDE_LAG_CYCLES)
+        launch()
+    for t in inputs:
+        t.record_stream(side)
+    store.hold_side(inputs)
+
+
 def _sink(w: torch.Tensor, produce, *inputs, defer: bool = False):
     """``produce(out, accumulate)`` writes the gradient of ``w``; returns what autograd should receive.
 
@@ -470,6 +495,11 @@ class _Norm(Function):
             # also write dx^T: the dY operand of the weight gradient of the projection that produced x
             dx, dxt = lib.rms_norm_bwd_t(dy, s, w, rstd, dres, dw_buf, acc and not staged)
             ctx.box.put(dx, dxt)
+        elif _NORM_SIDE and mg_w is not None and not staged and _side_active(w):
+            # the weight / bias gradient fold (two column reductions) goes to the weight-gradient stream: it is not on
+            # the data-gradient chain, and there it no longer waits for CUs behind that stream's GEMMs
+            dx, part = lib.norm_bwd_parts(dy, s, w, rstd, mean, dres, ctx.layernorm)
+            _side_launch(w, lambda: lib.norm_bwd_reduce_(part, dw_buf, db_buf, ctx.layernorm, acc), part)
         else:
             dx = lib.norm_bwd(dy, s, w, rstd, mean, dres, dw_buf, db_buf, ctx.layernorm, acc and not staged)
         if staged:

@@ -25,7 +25,7 @@ import os
 import time
 from typing import Any
 
-from fastapi import APIRouter, FastAPI, Request, WebSocket, WebSocketDisconnect
+from fastapi import APIRouter, Depends, FastAPI, Request, WebSocket, WebSocketDisconnect
 from fastapi.responses import FileResponse, JSONResponse, PlainTextResponse, RedirectResponse, Response
 from sqlalchemy import select
 
@@ -83,7 +83,14 @@ def superuser(request: Request) -> M.User:
     return u
 
 
+async def raw_body(request: Request) -> bytes:
+    return await request.body()
+
+
 async def body(request: Request) -> dict:
+    """The request's JSON (or form) payload. Handlers take it as a ``Depends(body)`` parameter and are plain
+    ``def`` functions, so FastAPI runs their blocking store / SSH / password-hash work in its thread pool
+    instead of on the event loop that serves every websocket."""
     raw = await request.body()
     if not raw:
         return {}
@@ -200,9 +207,8 @@ def crud(router: APIRouter, path: str, model, rtype: str | None = None, secrets:
         return paginate(request, rows) if paginated or "page" in request.query_params else rows
 
     @router.post(path, status_code=201)
-    async def _create(request: Request):
+    def _create(request: Request, data: dict = Depends(body)):
         u = superuser(request) if admin_write else current_user(request)
-        data = await body(request)
         with session_scope() as s:
             if "name" in cols and data.get("name") and s.scalar(select(model).where(model.name == data["name"])):
                 raise HTTPError(400, {"name": [f"{model.__name__} with this name already exists."]})
@@ -222,9 +228,8 @@ def crud(router: APIRouter, path: str, model, rtype: str | None = None, secrets:
         current_user(request)
         return render(_row(model, rid))
 
-    async def _update(rid: str, request: Request):
+    def _update(rid: str, request: Request, data: dict = Depends(body)):
         superuser(request) if admin_write else current_user(request)
-        data = await body(request)
         r = _row(model, rid)
         with session_scope() as s:
             row = s.get(model, r.id)
@@ -282,13 +287,11 @@ def create_app() -> FastAPI:
 
     # ------------------------------------------------------------------ users / auth (users/urls.py:13-23)
     @r.post("/token/auth/")
-    async def token_auth(request: Request):
-        d = await body(request)
+    def token_auth(request: Request, d: dict = Depends(body)):
         return users.authenticate(d.get("username", ""), d.get("password", ""))
 
     @r.post("/token/refresh/")
-    async def token_refresh(request: Request):
-        d = await body(request)
+    def token_refresh(request: Request, d: dict = Depends(body)):
         return users.refresh(d.get("token", ""))
 
     @r.get("/profile/")
@@ -296,9 +299,8 @@ def create_app() -> FastAPI:
         return users.profile(current_user(request))
 
     @r.put("/profile/")
-    async def update_profile(request: Request):
+    def update_profile(request: Request, d: dict = Depends(body)):
         u = current_user(request)
-        d = await body(request)
         with session_scope() as s:
             row = s.get(M.User, u.id)
             if "email" in d:
@@ -308,9 +310,8 @@ def create_app() -> FastAPI:
         return users.profile(_row(M.User, u.id))
 
     @r.put("/password/")
-    async def change_password(request: Request):
+    def change_password(request: Request, d: dict = Depends(body)):
         u = current_user(request)
-        d = await body(request)
         users.set_password(u.id, d.get("original"), d["password"])
         return {"msg": "ok"}
 
@@ -322,9 +323,8 @@ def create_app() -> FastAPI:
         return paginate(request, [users.profile(u) for u in rows])
 
     @r.post("/users/", status_code=201)
-    async def create_user(request: Request):
+    def create_user(request: Request, d: dict = Depends(body)):
         superuser(request)
-        d = await body(request)
         return users.create_user(d["username"], d.get("password", ""), d.get("email", ""),
                                  bool(d.get("is_superuser", False)))
 
@@ -335,9 +335,8 @@ def create_app() -> FastAPI:
 
     @r.put("/users/{uid}/")
     @r.patch("/users/{uid}/")
-    async def update_user(uid: str, request: Request):
+    def update_user(uid: str, request: Request, d: dict = Depends(body)):
         superuser(request)
-        d = await body(request)
         u = _user(uid)
         with session_scope() as s:
             row = s.get(M.User, u.id)
@@ -387,9 +386,8 @@ def create_app() -> FastAPI:
         return paginate(request, data)
 
     @r.post("/clusters/", status_code=201)
-    async def create_cluster(request: Request):
+    def create_cluster(request: Request, d: dict = Depends(body)):
         u = current_user(request)
-        d = await body(request)
         if not u.is_superuser:
             item = d.get("item_name")
             with session_scope() as s:
@@ -407,9 +405,8 @@ def create_app() -> FastAPI:
 
     @r.patch("/clusters/{name}/")
     @r.put("/clusters/{name}/")
-    async def update_cluster(name: str, request: Request):
+    def update_cluster(name: str, request: Request, d: dict = Depends(body)):
         c = _cluster_for(current_user(request), name, manage=True)
-        d = await body(request)
         with session_scope() as s:
             row = s.get(M.Cluster, c.id)
             for k in ("comment", "worker_size", "persistent_storage", "cluster_doamin_suffix"):
@@ -433,9 +430,8 @@ def create_app() -> FastAPI:
         return [{"key": k, "value": v} for k, v in (c.configs or {}).items()]
 
     @r.post("/clusters/{name}/configs/", status_code=201)
-    async def set_config(name: str, request: Request):
+    def set_config(name: str, request: Request, d: dict = Depends(body)):
         c = _cluster_for(current_user(request), name, manage=True)
-        d = await body(request)
         clusters.set_config(c.name, d["key"], d.get("value"))
         return {"key": d["key"], "value": d.get("value")}
 
@@ -447,9 +443,8 @@ def create_app() -> FastAPI:
         return {"key": key, "value": c.configs[key]}
 
     @r.put("/clusters/{name}/configs/{key}/")
-    async def put_config_key(name: str, key: str, request: Request):
+    def put_config_key(name: str, key: str, request: Request, d: dict = Depends(body)):
         c = _cluster_for(current_user(request), name, manage=True)
-        d = await body(request)
         clusters.set_config(c.name, key, d.get("value"))
         return {"key": key, "value": d.get("value")}
 
@@ -465,9 +460,9 @@ def create_app() -> FastAPI:
         return paginate(request, clusters.list_nodes(c.name))
 
     @r.post("/clusters/{name}/nodes/", status_code=201)
-    async def add_node(name: str, request: Request):
+    def add_node(name: str, request: Request, _data: dict = Depends(body)):
         c = _cluster_for(current_user(request), name, manage=True)
-        return clusters.add_node(c.name, await body(request))
+        return clusters.add_node(c.name, _data)
 
     @r.get("/clusters/{name}/nodes/{node}/")
     def get_node(name: str, node: str, request: Request):
@@ -507,10 +502,9 @@ def create_app() -> FastAPI:
         return paginate(request, [_exec_dict(e) for e in rows])
 
     @r.post("/clusters/{name}/executions/", status_code=201)
-    async def create_execution(name: str, request: Request):
+    def create_execution(name: str, request: Request, d: dict = Depends(body)):
         u = current_user(request)
         c = _cluster_for(u, name, manage=True)
-        d = await body(request)
         return deploy.create(c.name, d.get("operation", ""), d.get("params") or {}, user=u.username)
 
     def _own_execution(name: str, eid: str, request: Request):
@@ -656,9 +650,8 @@ def create_app() -> FastAPI:
         return monitor.node_time_skew(c.name)
 
     @r.post("/cluster/{name}/event/")
-    async def cluster_events(name: str, request: Request):
+    def cluster_events(name: str, request: Request, d: dict = Depends(body)):
         c = _cluster_for(current_user(request), name)
-        d = await body(request)
         return monitor.search_events(c.name, limit=int(d.get("limit", 100)), offset=int(d.get("offset", 0)),
                                      type_=d.get("type"))
 
@@ -709,9 +702,8 @@ def create_app() -> FastAPI:
         return paginate(request, _visible(u, "HOST", [hosts.host_dict(i) for i in ids]))
 
     @r.post("/host/", status_code=201)
-    async def create_host(request: Request):
+    def create_host(request: Request, d: dict = Depends(body)):
         u = current_user(request)
-        d = await body(request)
         out = hosts.create_host(d, check_ssh=bool(d.get("check_ssh", True)))
         if d.get("item_name"):
             users.add_item_resources(d["item_name"], "HOST", [out["id"]])
@@ -746,9 +738,8 @@ def create_app() -> FastAPI:
         return Response(status_code=204)
 
     @r.post("/host/import/")
-    async def import_hosts(request: Request):
+    def import_hosts(request: Request, raw: bytes = Depends(raw_body)):
         superuser(request)
-        raw = await request.body()
         ctype = request.headers.get("content-type", "")
         if ctype.startswith("multipart/"):
             parts = parse_multipart(ctype, raw)
@@ -758,9 +749,8 @@ def create_app() -> FastAPI:
         return hosts.import_hosts(fname or "hosts.csv", data, check_ssh=request.query_params.get("check_ssh") != "false")
 
     @r.post("/file/upload/")
-    async def upload_file(request: Request):
+    def upload_file(request: Request, raw: bytes = Depends(raw_body)):
         current_user(request)
-        raw = await request.body()
         ctype = request.headers.get("content-type", "")
         parts = parse_multipart(ctype, raw) if ctype.startswith("multipart/") else {"file": ("upload.bin", raw)}
         up = os.path.join(get_config().data_dir, "uploads")
@@ -781,9 +771,8 @@ def create_app() -> FastAPI:
 
     @r.post("/backupStorage/check")
     @r.post("/backupStorage/check/")
-    async def check_storage(request: Request):
+    def check_storage(request: Request, d: dict = Depends(body)):
         current_user(request)
-        d = await body(request)
         try:
             return {"message": "OK" if backup.client_for(d).check() else "FAILED"}
         except Exception as e:  # noqa: BLE001
@@ -791,9 +780,8 @@ def create_app() -> FastAPI:
 
     @r.post("/backupStorage/getBuckets")
     @r.post("/backupStorage/getBuckets/")
-    async def get_buckets(request: Request):
+    def get_buckets(request: Request, d: dict = Depends(body)):
         current_user(request)
-        d = await body(request)
         return backup.client_for(d).list_buckets()
 
     crud(r, "/backupStrategy/", M.BackupStrategy, admin_write=False)
@@ -823,9 +811,8 @@ def create_app() -> FastAPI:
 
     @r.put("/clusterBackup/restore/")
     @r.post("/clusterBackup/restore/")
-    async def restore_backup(request: Request):
+    def restore_backup(request: Request, d: dict = Depends(body)):
         u = current_user(request)
-        d = await body(request)
         b = _row(M.ClusterBackup, d.get("id") or d["clusterBackupId"])
         c = _cluster_for(u, b.cluster_id, manage=True)
         return deploy.create(c.name, "restore", {"clusterBackupId": b.id}, user=u.username)
@@ -842,9 +829,8 @@ def create_app() -> FastAPI:
                     for m in s.scalars(select(M.ItemRoleMapping).where(M.ItemRoleMapping.item_id == it.id))]
 
     @r.post("/item/profiles/{item}/")
-    async def set_item_profiles(item: str, request: Request):
+    def set_item_profiles(item: str, request: Request, d: dict = Depends(body)):
         superuser(request)
-        d = await body(request)
         it = _row(M.Item, item)
         users.set_item_profiles(it.name, d if isinstance(d, list) else d.get("profiles", []))
         return item_profiles(item, request)
@@ -866,9 +852,8 @@ def create_app() -> FastAPI:
         return [x for x in item_resources(item, request) if x["resource_type"] == rtype.upper()]
 
     @r.post("/resource/{item}/{rtype}/")
-    async def add_item_resources(item: str, rtype: str, request: Request):
+    def add_item_resources(item: str, rtype: str, request: Request, d: dict = Depends(body)):
         superuser(request)
-        d = await body(request)
         it = _row(M.Item, item)
         users.add_item_resources(it.name, rtype.upper(), d if isinstance(d, list) else d.get("ids", []))
         return item_resources_type(item, rtype, request)
@@ -892,9 +877,8 @@ def create_app() -> FastAPI:
 
     @r.post("/settings")
     @r.post("/settings/")
-    async def set_settings(request: Request):
+    def set_settings(request: Request, d: dict = Depends(body)):
         superuser(request)
-        d = await body(request)
         context.set_settings(d, tab=request.query_params.get("tab", "system"))
         return context.get_settings(request.query_params.get("tab"))
 
@@ -908,9 +892,8 @@ def create_app() -> FastAPI:
         return {"id": "dns", "dns1": st.get("dns1", ""), "dns2": st.get("dns2", "")}
 
     @r.post("/dns/update/")
-    async def update_dns(request: Request):
+    def update_dns(request: Request, d: dict = Depends(body)):
         superuser(request)
-        d = await body(request)
         vals = {k: str(d.get(k) or "").strip() for k in ("dns1", "dns2")}
         for k, v in vals.items():
             if v and not _is_ipv4(v):
@@ -929,9 +912,9 @@ def create_app() -> FastAPI:
     crud(r, "/plans/", M.Plan, rtype="PLAN")
 
     @r.post("/cloud/region/")
-    async def cloud_regions(request: Request):
+    def cloud_regions(request: Request, _data: dict = Depends(body)):
         current_user(request)
-        return cloud.list_regions_from_cloud(await body(request))
+        return cloud.list_regions_from_cloud(_data)
 
     @r.get("/cloud/compute/")
     def compute_models(request: Request):
@@ -957,9 +940,9 @@ def create_app() -> FastAPI:
         return storage.list_nfs()
 
     @r.post("/storage/nfs/", status_code=201)
-    async def create_nfs(request: Request):
+    def create_nfs(request: Request, _data: dict = Depends(body)):
         superuser(request)
-        return storage.create_nfs(await body(request))
+        return storage.create_nfs(_data)
 
     @r.delete("/storage/nfs/{name}/", status_code=204)
     def delete_nfs(name: str, request: Request):
@@ -973,9 +956,9 @@ def create_app() -> FastAPI:
         return storage.list_ceph()
 
     @r.post("/storage/ceph/", status_code=201)
-    async def create_ceph(request: Request):
+    def create_ceph(request: Request, _data: dict = Depends(body)):
         superuser(request)
-        return storage.create_ceph(await body(request))
+        return storage.create_ceph(_data)
 
     @r.delete("/storage/ceph/{name}/", status_code=204)
     def delete_ceph(name: str, request: Request):
@@ -985,9 +968,8 @@ def create_app() -> FastAPI:
 
     # ------------------------------------------------------------------ logs / notifications
     @r.post("/log/")
-    async def search_log(request: Request):
+    def search_log(request: Request, d: dict = Depends(body)):
         current_user(request)
-        d = await body(request)
         return monitor.search_system_log(d.get("level"), d.get("keywords"), int(d.get("days", 7)),
                                          int(d.get("limit", 50)), int(d.get("offset", 0)))
 
@@ -1000,9 +982,8 @@ def create_app() -> FastAPI:
 
     @r.put("/notification/subscribe/")
     @r.post("/notification/subscribe/")
-    async def set_subscribe(request: Request):
+    def set_subscribe(request: Request, d: dict = Depends(body)):
         u = current_user(request)
-        d = await body(request)
         with session_scope() as s:
             row = s.scalar(select(M.UserNotificationConfig).where(M.UserNotificationConfig.user_id == u.id,
                                                                   M.UserNotificationConfig.type == d.get("type", "SYSTEM")))
@@ -1021,9 +1002,8 @@ def create_app() -> FastAPI:
 
     @r.put("/notification/receiver/")
     @r.post("/notification/receiver/")
-    async def set_receiver(request: Request):
+    def set_receiver(request: Request, d: dict = Depends(body)):
         u = current_user(request)
-        d = await body(request)
         with session_scope() as s:
             row = s.scalar(select(M.UserReceiver).where(M.UserReceiver.user_id == u.id))
             if row is None:
@@ -1042,9 +1022,8 @@ def create_app() -> FastAPI:
 
     @r.put("/notification/userMessage/")
     @r.post("/notification/userMessage/read/")
-    async def mark_messages(request: Request):
+    def mark_messages(request: Request, d: dict = Depends(body)):
         u = current_user(request)
-        d = await body(request)
         ids = d if isinstance(d, list) else d.get("ids")
         return {"updated": messages.mark_read(u.id, ids)}
 
@@ -1053,17 +1032,15 @@ def create_app() -> FastAPI:
         return {"unread": messages.unread_count(current_user(request).id)}
 
     @r.post("/notification/email/check/")
-    async def check_email(request: Request):
+    def check_email(request: Request, d: dict = Depends(body)):
         superuser(request)
-        d = await body(request)
         ok = messages.send_email(d, d.get("SMTP_TEST_USER") or d.get("SMTP_USERNAME", ""), "KubeOperator test",
                                  "test message")
         return {"success": ok}
 
     @r.post("/notification/workWeixin/check/")
-    async def check_ww(request: Request):
+    def check_ww(request: Request, d: dict = Depends(body)):
         superuser(request)
-        d = await body(request)
         try:
             return {"success": messages.send_workweixin(d, d.get("WORKWEIXIN_TEST_USER", "@all"), "KubeOperator test")}
         except Exception as e:  # noqa: BLE001

@@ -468,8 +468,7 @@ class Local:
     def operate(self, name, op, params):
         from .runtime import jobs
 
-        e = self.deploy.create(name, op, params, user="kubeopsctl", run="none")
-        jobs.submit("start_deploy_execution", {"execution_id": e["id"]}, job_id=e["id"])
+        e = self.deploy.create(name, op, params, user="kubeopsctl", run="claim")
         path = jobs.log_path(e["id"])
         import threading
 
@@ -488,7 +487,7 @@ class Local:
         open(path, "a").close()
         t = threading.Thread(target=follow, daemon=True)
         t.start()
-        jobs.run_job(jobs._claim_specific(e["id"]))
+        jobs.run_claimed(jobs.get(e["id"]))
         done.set()
         t.join(5)
         return self.deploy.get(e["id"])

@@ -8,9 +8,9 @@ resource/clouds/*/terraform/terraform.tf.j2, compute_model_meta.yml.
 Providers: ``vsphere`` and ``openstack`` render ``resources/clouds/<provider>/terraform/main.tf.j2`` and run
 the ``terraform`` binary (streamed to the execution log); ``baremetal`` allocates idle registered hosts
 (e.g. 8x MI355X servers) from the zone's pool instead of creating VMs; ``fake`` renders the Terraform file
-and returns the planned hosts without calling any API (CI). IP allocation is transactional (a process lock
-around the zone's read-modify-write; the reference's ``Zone.allocate_ip`` could double-allocate under
-concurrent installs).
+and returns the planned hosts without calling any API (CI). IP allocation is transactional (the zone's read-modify-write
+runs under the store's write lock, ``store.db.write_scope``, so allocators in other threads and processes are
+serialised; the reference's ``Zone.allocate_ip`` could double-allocate under concurrent installs).
 """
 from __future__ import annotations
 
@@ -18,7 +18,6 @@ import ipaddress
 import os
 import shutil
 import subprocess
-import threading
 
 import jinja2
 import yaml
@@ -27,10 +26,8 @@ from sqlalchemy import select
 from ..conf import RESOURCE_DIR, get_config
 from ..runtime import jobs
 from ..store import models as M
-from ..store.db import session_scope
+from ..store.db import session_scope, write_scope
 from . import clusters
-
-_ip_lock = threading.Lock()
 
 
 def _provider_meta(provider: str) -> dict:
@@ -80,8 +77,11 @@ def zone_provider(s, zone: M.Zone) -> str:
 
 
 def allocate_ip(zone_id: str) -> str:
-    with _ip_lock, session_scope() as s:
-        z = s.get(M.Zone, zone_id)
+    """Take the zone's first free address. The zone row's read-modify-write runs under the store's write lock
+    (``write_scope``: BEGIN IMMEDIATE on SQLite, SELECT ... FOR UPDATE elsewhere), so concurrent allocators in
+    other threads or processes never hand out one address twice."""
+    with write_scope() as s:
+        z = s.get(M.Zone, zone_id, with_for_update=True)
         pool = ip_pool(z, zone_provider(s, z))
         if not pool:
             raise RuntimeError(f"zone {z.name}: no available ip address")
@@ -91,8 +91,8 @@ def allocate_ip(zone_id: str) -> str:
 
 
 def recover_ip(zone_id: str, ip: str) -> None:
-    with _ip_lock, session_scope() as s:
-        z = s.get(M.Zone, zone_id)
+    with write_scope() as s:
+        z = s.get(M.Zone, zone_id, with_for_update=True)
         z.ip_used = [x for x in (z.ip_used or []) if x != ip]
 
 

@@ -29,12 +29,13 @@ import re
 import time
 
 from sqlalchemy import select
+from sqlalchemy.exc import IntegrityError
 
 from ..engine.trace import Tracer, chrome_trace
 from ..engine.trace import summary as trace_summary
 from ..runtime import jobs, metrics
 from ..store import models as M
-from ..store.db import session_scope
+from ..store.db import session_scope, write_scope
 from . import clusters, context, plan
 
 log = logging.getLogger("kubeoperator.deploy")
@@ -56,37 +57,52 @@ OPERATION_NAME = {"install": "Cluster install", "uninstall": "Cluster uninstall"
 
 def create(cluster_name: str, operation: str, params: dict | None = None, user: str = "",
            run: str = "queue") -> dict:
-    """Create a DeployExecution and start it (``run``: queue | inline | none)."""
+    """Create a DeployExecution and start it. ``run``: ``queue`` (a worker runs it), ``inline`` (run it here and
+    return when done), ``claim`` (its job is created STARTED and owned by the caller, which runs it with
+    ``jobs.run_claimed(jobs.get(id))``), ``none`` (no job; such an execution does not lock the cluster)."""
     if operation not in OPERATIONS:
         raise ValueError(f"unknown operation {operation!r}; one of {OPERATIONS}")
     c = clusters.get_cluster(cluster_name)
     params = dict(params or {})
     if operation in ("app-deploy", "app-remove"):
         _check_app_params(operation, params)
-    with session_scope() as s:
-        busy = s.scalar(select(M.Execution).where(M.Execution.project_id == c.project_id, M.Execution.kind == "deploy",
-                                                  M.Execution.state.in_(("PENDING", "STARTED"))))
-        if busy is not None and _stale(s, busy):
-            busy.state, busy.date_end = "FAILURE", M.now()
-            busy.result_summary = {"error": "abandoned: no job was ever run for this execution"}
-            busy = None
-        if busy is not None:
-            raise clusters.Conflict(f"cluster {cluster_name} is busy with {busy.operation} ({busy.id})")
-        if c.deploy_type == "AUTOMATIC" and operation in ("install", "scale"):
-            from . import cloud
+    if c.deploy_type == "AUTOMATIC" and operation in ("install", "scale"):
+        from . import cloud
 
-            need = len(clusters.list_nodes(cluster_name)) if operation == "install" else int(params.get("num", 0))
-            cloud.check_capacity(c, need)
-        steps = [dict(st, status="pending") for st in plan.operation_steps(operation)]
-        e = M.Execution(kind="deploy", project_id=c.project_id, operation=operation, params=params, steps=steps,
-                        state="PENDING", created_by=user)
-        s.add(e)
-        s.flush()
-        eid = e.id
+        need = len(clusters.list_nodes(cluster_name)) if operation == "install" else int(params.get("num", 0))
+        cloud.check_capacity(c, need)
+    steps = [dict(st, status="pending") for st in plan.operation_steps(operation)]
+    # Check-and-insert under the store's write lock (BEGIN IMMEDIATE on SQLite), backed by the partial unique
+    # index uq_one_active_deploy_per_project: two creators -- API threads, the scheduled backup's worker thread,
+    # a CLI process on the same store -- can never both pass the busy check.
+    try:
+        with write_scope() as s:
+            busy = s.scalar(select(M.Execution).where(M.Execution.project_id == c.project_id,
+                                                      M.Execution.kind == "deploy",
+                                                      M.Execution.state.in_(("PENDING", "STARTED")))
+                            .with_for_update())
+            if busy is not None and _stale(s, busy):
+                busy.state, busy.date_end = "FAILURE", M.now()
+                busy.result_summary = {"error": "abandoned: no job was ever run for this execution"}
+                s.flush()
+                busy = None
+            if busy is not None:
+                raise clusters.Conflict(f"cluster {cluster_name} is busy with {busy.operation} ({busy.id})")
+            e = M.Execution(kind="deploy", project_id=c.project_id, operation=operation, params=params, steps=steps,
+                            state="PENDING", created_by=user)
+            s.add(e)
+            s.flush()
+            eid = e.id
+            # The execution's job commits in the same transaction: there is no window in which a concurrent
+            # creator sees a job-less execution and takes it for abandoned (``_stale``).
+            job = None if run == "none" else jobs.add_job(s, "start_deploy_execution", {"execution_id": eid},
+                                                          job_id=eid, inline=run in ("inline", "claim"))
+    except IntegrityError as err:
+        raise clusters.Conflict(f"cluster {cluster_name} is busy with another operation") from err
     if run == "queue":
-        jobs.submit("start_deploy_execution", {"execution_id": eid}, job_id=eid)
+        jobs.wake()
     elif run == "inline":
-        jobs.run_inline("start_deploy_execution", {"execution_id": eid}, job_id=eid)
+        jobs.run_claimed(job)
     return get(eid)
 
 
@@ -94,7 +110,7 @@ def _stale(s, e: M.Execution) -> bool:
     """A PENDING/STARTED execution whose job is missing or finished (e.g. a client died between creating the
     execution and queueing it) must not lock the cluster forever."""
     j = s.get(M.Job, e.id)
-    return j is None or j.state in ("SUCCESS", "FAILURE")
+    return j is None or j.state in ("SUCCESS", "FAILURE", "REVOKED")
 
 
 def get(execution_id: str) -> dict:

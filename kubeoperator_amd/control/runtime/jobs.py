@@ -6,9 +6,12 @@ worker processes can share one store; ``WORKER_CONCURRENCY`` threads per process
 ``-c 4``). Each job's log goes to ``<DATA_DIR>/celery/<id[0]>/<id[1]>/<id>.log`` -- the reference's path
 convention (celery_api/utils.py:212-217) -- which the log API / websocket tail.
 
-Recovery: at worker start every job left STARTED by a dead worker is marked FAILURE (and its
-execution too), instead of the reference's "mark the previous STARTED execution FAILURE when a new one
-starts" (kubeops_api/api.py:244-248).
+Recovery: a job left STARTED by a DEAD worker is marked FAILURE, together with the execution of the same id,
+instead of the reference's "mark the previous STARTED execution FAILURE when a new one starts"
+(kubeops_api/api.py:244-248). Every runner -- pool workers and inline runs (CLI, ``run_inline``) alike -- owns a
+heartbeat row; a worker counts as dead when its row is missing, its pid is gone on this host, or it has not
+beaten for ``3 x heartbeat_s``. A live worker's jobs are never touched, so a second worker process starting on
+the same store cannot unlock a cluster whose operation is still running.
 
 Task monitor (the reference runs Celery Flower, core/kubeops.py:197-213, proxied at /flower/): every worker
 process keeps a heartbeat row (jobs running, jobs processed, last seen); ``stats`` aggregates the job table per
@@ -89,13 +92,35 @@ def tail(path: str, offset: int = 0, limit: int = 4096) -> tuple[str, int]:
     return data.decode(errors="replace"), offset + len(data)
 
 
-def submit(name: str, args: dict | None = None, job_id: str | None = None) -> str:
+def add_job(s, name: str, args: dict | None = None, job_id: str | None = None, inline: bool = False) -> M.Job:
+    """Add a job row inside the caller's transaction ``s`` (so e.g. an execution and its job commit together).
+    ``inline=True``: the row is born STARTED and owned by a fresh inline worker with its own heartbeat row, so no
+    pool worker can claim it between insert and run; run it with ``run_claimed``."""
     if name not in _TASKS:
         raise KeyError(f"unknown task {name!r}")
     jid = job_id or str(uuid.uuid4())
-    with session_scope() as s:
-        s.add(M.Job(id=jid, name=name, args=args or {}, state="PENDING", log_path=log_path(jid)))
+    if inline:
+        t = M.now()
+        wname = f"inline:{socket.gethostname()}:{os.getpid()}:{uuid.uuid4().hex[:8]}"
+        s.add(M.WorkerHeartbeat(name=wname, hostname=socket.gethostname(), pid=os.getpid(), concurrency=1,
+                                started=t, last_seen=t, active=[jid], processed=0, stopped=False))
+        job = M.Job(id=jid, name=name, args=args or {}, state="STARTED", worker=wname, date_start=t, attempts=1,
+                    log_path=log_path(jid))
+    else:
+        job = M.Job(id=jid, name=name, args=args or {}, state="PENDING", log_path=log_path(jid))
+    s.add(job)
+    return job
+
+
+def wake() -> None:
+    """Tell this process's idle workers that a job was queued (other processes find it on their next poll)."""
     _wake.set()
+
+
+def submit(name: str, args: dict | None = None, job_id: str | None = None) -> str:
+    with session_scope() as s:
+        jid = add_job(s, name, args, job_id).id
+    wake()
     return jid
 
 
@@ -195,25 +220,102 @@ def run_job(job: M.Job) -> dict:
 
 
 def run_inline(name: str, args: dict | None = None, job_id: str | None = None) -> dict:
-    """Submit and execute in the calling thread (tests, CLI, single-process mode)."""
-    jid = submit(name, args, job_id)
-    job = _claim_specific(jid)
-    return {"id": jid, **run_job(job)}
-
-
-def _claim_specific(jid: str) -> M.Job:
+    """Execute a new job in the calling thread (tests, CLI, single-process mode)."""
     with session_scope() as s:
-        s.execute(update(M.Job).where(M.Job.id == jid).values(state="STARTED", worker="inline", date_start=M.now()))
+        job = add_job(s, name, args, job_id, inline=True)
+    return {"id": job.id, **run_claimed(job)}
+
+
+INLINE_HEARTBEAT_S = 5.0
+
+
+def claim_pending(jid: str) -> M.Job:
+    """Claim one PENDING job for the calling thread (an inline worker with a heartbeat row, as ``add_job``'s
+    ``inline``); raises if a pool worker took it first. Run it with ``run_claimed``."""
+    name = f"inline:{socket.gethostname()}:{os.getpid()}:{uuid.uuid4().hex[:8]}"
+    with session_scope() as s:
+        n = s.execute(update(M.Job).where(M.Job.id == jid, M.Job.state == "PENDING")
+                      .values(state="STARTED", worker=name, date_start=M.now(), attempts=M.Job.attempts + 1)).rowcount
+        if n != 1:
+            raise RuntimeError(f"job {jid} is not PENDING")
+        s.add(M.WorkerHeartbeat(name=name, hostname=socket.gethostname(), pid=os.getpid(), concurrency=1,
+                                started=M.now(), last_seen=M.now(), active=[jid], processed=0, stopped=False))
+        s.flush()
         return s.get(M.Job, jid)
 
 
-def recover_orphans() -> int:
-    """Mark jobs/executions left STARTED by a dead worker as FAILURE; returns how many."""
+def run_claimed(job: M.Job, heartbeat_s: float = INLINE_HEARTBEAT_S) -> dict:
+    """``run_job`` for an inline-owned job (``add_job(inline=True)`` / ``claim_pending``): a daemon thread beats the inline worker's row
+    every ``heartbeat_s`` until the job ends, then the row is marked stopped."""
+    stop = threading.Event()
+
+    def beat(**extra):
+        with session_scope() as s:
+            s.execute(update(M.WorkerHeartbeat).where(M.WorkerHeartbeat.name == job.worker)
+                      .values(last_seen=M.now(), **extra))
+
+    def loop():
+        while not stop.wait(heartbeat_s):
+            try:
+                beat()
+            except Exception:  # noqa: BLE001 - a missed heartbeat is not fatal
+                log.exception("inline heartbeat failed")
+
+    t = threading.Thread(target=loop, name="kop-inline-heartbeat", daemon=True)
+    t.start()
+    try:
+        return run_job(job)
+    finally:
+        stop.set()
+        t.join(heartbeat_s + 1.0)
+        try:
+            beat(active=[], processed=1, stopped=True)
+        except Exception:  # noqa: BLE001
+            log.exception("inline heartbeat failed")
+
+
+def _pid_alive(pid: int) -> bool:
+    if pid <= 0:
+        return False
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+    return True
+
+
+def worker_dead(w: M.WorkerHeartbeat | None, now, stale_s: float) -> bool:
+    """The liveness rule orphan recovery applies to a job's worker row."""
+    if w is None:
+        return True
+    if w.hostname == socket.gethostname() and not _pid_alive(int(w.pid or 0)):
+        return True
+    return w.last_seen is None or (now - w.last_seen).total_seconds() > stale_s
+
+
+def recover_orphans(heartbeat_s: float = 5.0) -> int:
+    """Mark jobs left STARTED by a dead worker (see ``worker_dead``; stale after ``3 x heartbeat_s``) as
+    FAILURE, each together with its execution (same id). Jobs of live workers -- other pool processes, inline
+    runs -- are left alone. Returns how many jobs were failed."""
+    now = M.now()
+    n = 0
     with session_scope() as s:
-        n = s.execute(update(M.Job).where(M.Job.state == "STARTED")
-                      .values(state="FAILURE", result={"error": "worker died"}, date_end=M.now())).rowcount
-        s.execute(update(M.Execution).where(M.Execution.state == "STARTED")
-                  .values(state="FAILURE", date_end=M.now(), result_summary={"error": "worker died"}))
+        rows = list(s.execute(select(M.Job.id, M.Job.worker).where(M.Job.state == "STARTED")))
+        beats = {w.name: w for w in s.scalars(select(M.WorkerHeartbeat).where(
+            M.WorkerHeartbeat.name.in_({wk for _, wk in rows})))} if rows else {}
+        for jid, wk in rows:
+            if not worker_dead(beats.get(wk), now, 3.0 * heartbeat_s):
+                continue
+            err = {"error": f"worker died ({wk or 'unknown'})"}
+            k = s.execute(update(M.Job).where(M.Job.id == jid, M.Job.state == "STARTED", M.Job.worker == wk)
+                          .values(state="FAILURE", result=err, date_end=now)).rowcount
+            if k:
+                n += k
+                s.execute(update(M.Execution).where(M.Execution.id == jid,
+                                                    M.Execution.state.in_(("PENDING", "STARTED")))
+                          .values(state="FAILURE", date_end=now, result_summary=err))
     return n
 
 
@@ -235,10 +337,9 @@ class WorkerPool:
         self._lock = threading.Lock()
 
     def start(self, recover: bool = True):
+        self._recover = recover
         if recover:
-            n = recover_orphans()
-            if n:
-                log.warning("recovered %d orphaned jobs", n)
+            self._recover_orphans()
         with session_scope() as s:
             s.merge(M.WorkerHeartbeat(name=self.name, hostname=socket.gethostname(), pid=os.getpid(),
                                       concurrency=self.concurrency, started=M.now(), last_seen=M.now(), active=[],
@@ -267,10 +368,19 @@ class WorkerPool:
         except Exception:  # noqa: BLE001
             log.exception("worker heartbeat failed")
 
+    def _recover_orphans(self) -> None:
+        n = recover_orphans(self.heartbeat_s)
+        if n:
+            log.warning("recovered %d orphaned jobs", n)
+
     def _heartbeat_loop(self):
+        beats = 0
         while not self._stop.wait(self.heartbeat_s):
             try:
                 self._beat()
+                beats += 1
+                if self._recover and beats % 6 == 0:  # a worker that dies later is noticed without a restart
+                    self._recover_orphans()
             except Exception:  # noqa: BLE001 - a missed heartbeat is not fatal
                 log.exception("worker heartbeat failed")
 
@@ -297,7 +407,10 @@ class WorkerPool:
         _wake.set()
         for t in self._threads:
             t.join(timeout)
+        with self._lock:
+            busy = bool(self._active)
         try:
-            self._beat(stopped=True)
+            # A job still running in a (daemon) worker thread: the row is not marked stopped.
+            self._beat(stopped=not busy)
         except Exception:  # noqa: BLE001
             pass

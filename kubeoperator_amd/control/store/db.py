@@ -74,11 +74,50 @@ def session_scope():
         s.close()
 
 
+_write_lock = threading.RLock()
+
+
+@contextlib.contextmanager
+def write_scope():
+    """A session whose transaction takes the store's write lock before its first read, for read-check-write
+    sequences that must be atomic across threads AND processes (one active execution per cluster, IP
+    allocation). SQLite: ``BEGIN IMMEDIATE`` -- the write lock up front, so a second writer (another thread or
+    another process on the same file) waits in ``busy_timeout`` instead of interleaving its check with ours.
+    Other databases: the caller's ``with_for_update`` row locks do the same job. A process-local lock also
+    serialises threads that share one connection (the in-memory test store's single pooled connection, where
+    a nested ``BEGIN`` is not allowed). Replaces the reference's unlocked check-then-insert
+    (kubeops_api/api.py:244-248, cloud_provider/models.py:140-144)."""
+    with _write_lock:
+        s = session()
+        try:
+            conn = s.connection()
+            if conn.dialect.name == "sqlite":
+                dbapi = conn.connection.dbapi_connection
+                if not dbapi.in_transaction:
+                    conn.exec_driver_sql("BEGIN IMMEDIATE")
+            yield s
+            s.commit()
+        except Exception:
+            s.rollback()
+            raise
+        finally:
+            s.close()
+
+
+def ensure_indexes() -> None:
+    """Create indexes added after a store's tables were first created (``create_all`` skips existing tables)."""
+    eng = engine()
+    for t in M.Base.metadata.sorted_tables:
+        for ix in t.indexes:
+            ix.create(eng, checkfirst=True)
+
+
 def init_db(admin_password: str | None = None) -> None:
     from ..conf import get_config
 
     eng = engine()
     M.Base.metadata.create_all(eng)
+    ensure_indexes()
     cfg = get_config()
     with session_scope() as s:
         if s.get(M.SchemaVersion, SCHEMA_VERSION) is None:

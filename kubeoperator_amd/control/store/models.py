@@ -17,7 +17,8 @@ from __future__ import annotations
 import datetime as _dt
 import uuid
 
-from sqlalchemy import JSON, Boolean, DateTime, Float, ForeignKey, Integer, String, Text, UniqueConstraint
+from sqlalchemy import (JSON, Boolean, DateTime, Float, ForeignKey, Index, Integer, String, Text, UniqueConstraint,
+                        text)
 from sqlalchemy.orm import DeclarativeBase, Mapped, mapped_column
 
 
@@ -274,6 +275,11 @@ class Execution(IdMixin, Base):
     date_start: Mapped[_dt.datetime | None] = mapped_column(DateTime, nullable=True)
     date_end: Mapped[_dt.datetime | None] = mapped_column(DateTime, nullable=True)
     created_by: Mapped[str] = mapped_column(String(128), default="")
+    # At most one active (PENDING/STARTED) deploy execution per cluster, enforced by the database itself: a
+    # partial unique index (SQLite / PostgreSQL), so no interleaving of two creators can slip a second one in.
+    __table_args__ = (Index("uq_one_active_deploy_per_project", "project_id", unique=True,
+                            sqlite_where=text("kind = 'deploy' AND state IN ('PENDING', 'STARTED')"),
+                            postgresql_where=text("kind = 'deploy' AND state IN ('PENDING', 'STARTED')")),)
 
 
 # ------------------------------------------------------------------------------------------- backup

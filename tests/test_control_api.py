@@ -67,7 +67,7 @@ def test_cluster_lifecycle_over_http_and_ws(client):
     eid = r.json()["id"]
     # worker pool is not running in tests: execute the queued job in-process, then watch the progress socket
     from kubeoperator_amd.control.runtime import jobs
-    jobs.run_job(jobs._claim_specific(eid))
+    jobs.run_claimed(jobs.claim_pending(eid))
     tok = client.headers["Authorization"].split()[1]
     with pytest.raises(Exception):
         with TestClient(create_app()).websocket_connect(f"/ws/progress/{eid}/") as ws:
@@ -242,7 +242,7 @@ def test_app_catalog_and_deploy_over_http(client):
         "name": "demo", "template": "single-master", "item_name": "KubeOperator",
         "nodes": [{"name": "m1", "host": "m1", "roles": ["master"]}, {"name": "w1", "host": "w1", "roles": ["worker"]}]})
     eid = client.post("/api/v1/clusters/demo/executions/", json={"operation": "install"}).json()["id"]
-    jobs.run_job(jobs._claim_specific(eid))
+    jobs.run_claimed(jobs.claim_pending(eid))
     r = client.post("/api/v1/clusters/demo/executions/",
                     json={"operation": "app-deploy", "params": {"chart": "nginx", "release": "Bad Name"}})
     assert r.status_code == 400
@@ -250,7 +250,7 @@ def test_app_catalog_and_deploy_over_http(client):
                     json={"operation": "app-deploy", "params": {"chart": "pytorch-rocm-train", "release": "gpt2",
                                                                 "values": {"model": "gpt2_small"}, "wait_job": True}})
     assert r.status_code == 201, r.text
-    jobs.run_job(jobs._claim_specific(r.json()["id"]))
+    jobs.run_claimed(jobs.claim_pending(r.json()["id"]))
     e = client.get(f"/api/v1/clusters/demo/executions/{r.json()['id']}/").json()
     assert e["state"] == "SUCCESS" and e["result_summary"]["training"]["tokens_per_s"] > 0
     apps = client.get("/api/v1/clusters/demo/apps/").json()

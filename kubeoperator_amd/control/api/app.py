@@ -253,9 +253,31 @@ def crud(router: APIRouter, path: str, model, rtype: str | None = None, secrets:
 
 # ------------------------------------------------------------------------------------------------ app
 def create_app() -> FastAPI:
-    app = FastAPI(title="KubeOperator-AMD", version=__version__, docs_url="/swagger/", redoc_url=None,
+    # FastAPI's own /docs pages load swagger-ui from a CDN and render blank offline: the API explorer here is one
+    # self-contained page (api/explorer.html, no external assets), served where the reference serves its schema
+    # views (kubeoperator/urls.py:44-47): /swagger/, /docs/, /redoc/, plus the raw schema at /docs.json, /docs.yaml
+    app = FastAPI(title="KubeOperator-AMD", version=__version__, docs_url=None, redoc_url=None,
                   openapi_url="/swagger.json")
     r = APIRouter(prefix=API)
+
+    explorer = os.path.join(os.path.dirname(os.path.abspath(__file__)), "explorer.html")
+
+    def _explorer():
+        with open(explorer) as f:
+            return Response(f.read(), media_type="text/html")
+
+    for _p in ("/swagger/", "/docs/", "/redoc/"):
+        app.get(_p, include_in_schema=False)(_explorer)
+
+    @app.get("/docs.json", include_in_schema=False)
+    def docs_json():
+        return JSONResponse(app.openapi())
+
+    @app.get("/docs.yaml", include_in_schema=False)
+    def docs_yaml():
+        import yaml
+
+        return Response(yaml.safe_dump(app.openapi(), sort_keys=False), media_type="application/yaml")
 
     @app.exception_handler(HTTPError)
     async def _h1(_, e: HTTPError):

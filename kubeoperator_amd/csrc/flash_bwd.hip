@@ -1041,7 +1041,13 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
     const bool blk = one_wave && cfg != 66;
     bool done = false;
     int np = direct ? 0 : Hq / Hkv;  // fp32 partials per GQA group left for the finalize pass
-    if (one_wave) {
+    // cfg 68: the D = 64 dK/dV kernel with two waves per SIMD (flash_bwd_d64.hip), key-major dS tiles
+    const bool w2 = D == 64 && cfg == 68 && S % 256 == 0;
+    if (w2) {
+      np = flash_attn_bwd_dkdv_d64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs,
+                                   dos, dks, dvs, scale, cflag, stream);
+      done = true;
+    } else if (one_wave) {
       np = flash_attn_bwd_dkdv64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, D, qs, ks, vs,
                                  dos, dks, dvs, scale, cflag, !kmaj, blk, stream);
       done = true;
@@ -1061,7 +1067,7 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
     if (!done)
       launch_dkdv_ds<D, NW, 2>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs,
                                dos, dks, dvs, scale, cflag, stream);
-    if (one_wave && kmaj) launch_dq_ds_hp<D, false, true>(hp, ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+    if ((one_wave && kmaj) || w2) launch_dq_ds_hp<D, false, true>(hp, ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
     else if (blk) launch_dq_ds_hp<D, true>(hp, ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
     else launch_dq_ds_hp<D, false>(hp, ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
     if (np > 0) fa_bwd_finalize_kernel<D><<<2048, 256, 0, stream>>>(dk_part, dv_part, dk, dv, T, Hq, Hkv, dks, dvs, np);

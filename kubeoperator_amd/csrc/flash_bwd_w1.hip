@@ -10,17 +10,6 @@
 
 namespace kop {
 
-// 16-byte LDS read (4 floats) at a lane base + immediate, retired by the caller's counted lgkmcnt
-template <int OFF>
-__device__ __forceinline__ f32x4 lds_read16f_off(uint32_t base) {
-  f32x4 r;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(base), "n"(OFF));
-  return r;
-}
-__device__ __forceinline__ f32x16 cat4f(const f32x4* q) {
-  return f32x16{q[0][0], q[0][1], q[0][2], q[0][3], q[1][0], q[1][1], q[1][2], q[1][3],
-                q[2][0], q[2][1], q[2][2], q[2][3], q[3][0], q[3][1], q[3][2], q[3][3]};
-}
 
 // QM staging write: lane r holds key r (of the block at byte offset BLK), queries 16S + {0-3, 8-11} (+4 for hh = 1);
 // one permlane32_swap per dword pairs the halves into queries 16S + 8hh .. +7 (16 B) -> one ds_write_b128
@@ -77,21 +66,6 @@ __device__ __forceinline__ void mfma32_agpr(f32x16& acc, bf16x8 a, bf16x8 b) {
 //     4-query runs per register quad, so one v_permlane32_swap per dword pairs the two lane halves into
 //     8-query (16 B) runs -- 4 dwordx4 stores per wave per stage instead of 32 two-byte stores.
 // Stage ring: Q / dO / {-lse/scale, -delta} of 32 queries, NS deep, behind counted vmcnt + raw barriers.
-#define KOP_VM_CASE(n) \
-  case n:              \
-    asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); \
-    break;
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n (0..15)
-__device__ __forceinline__ void vm_wait_le(int n) {
-  switch (n) {
-    KOP_VM_CASE(0) KOP_VM_CASE(1) KOP_VM_CASE(2) KOP_VM_CASE(3) KOP_VM_CASE(4) KOP_VM_CASE(5) KOP_VM_CASE(6)
-    KOP_VM_CASE(7) KOP_VM_CASE(8) KOP_VM_CASE(9) KOP_VM_CASE(10) KOP_VM_CASE(11) KOP_VM_CASE(12) KOP_VM_CASE(13)
-    KOP_VM_CASE(14)
-    default:
-      asm volatile("s_waitcnt vmcnt(15)" ::: "memory");
-  }
-}
-#undef KOP_VM_CASE
 
 // DIAG bit 1: no dS stores -- the build the recompute-dQ path (KOP_DQ_VARIANT 9) launches. Timing ablations
 // (KOP_DKDV64_DIAG, wrong results): 2 no exponentials, 4 no stage DMA, 8 no stage barrier, 32 no DMA wait; 16

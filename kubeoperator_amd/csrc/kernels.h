@@ -99,6 +99,12 @@ int flash_attn_bwd_dkdv64(const bf16_t* q, const bf16_t* k, const bf16_t* v, con
                            const float* ndelta, float* dk_part, float* dv_part, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B,
                            int S, int Hq, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t dos, int64_t dks,
                            int64_t dvs, float scale, int causal, bool qm, bool blk_layout, hipStream_t stream);
+// dK/dV at D = 64 with two waves per SIMD (flash_bwd_d64.hip), S % 256 == 0; dS in the key-major tiles of
+// fa_bwd_dq_ds_kernel<KMAJ>. Returns the fp32 partials per GQA group left for the finalize pass (0: bf16 dK / dV written).
+int flash_attn_bwd_dkdv_d64(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout, const float* nlse,
+                            const float* ndelta, float* dk_part, float* dv_part, bf16_t* dk, bf16_t* dv, bf16_t* ds,
+                            int B, int S, int Hq, int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t dos, int64_t dks,
+                            int64_t dvs, float scale, int causal, hipStream_t stream);
 int flash_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
                    const float* lse, bf16_t* dq, bf16_t* dk, bf16_t* dv, void* workspace, int B, int S, int Hq,
                    int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, int64_t dos, int64_t dqs,

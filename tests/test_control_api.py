@@ -214,6 +214,28 @@ def test_ui_served(control):
     assert r.status_code == 200 and "<html" in r.text.lower()
 
 
+def test_api_explorer_is_offline(control):
+    """/swagger/, /docs/ and /redoc/ serve one self-contained explorer page (no http(s) asset URL: the offline
+    install has no CDN) that reads the schema from this server; /docs.json and /docs.yaml serve the schema itself
+    (reference kubeoperator/urls.py:44-47)."""
+    import re
+
+    import yaml
+
+    c = TestClient(create_app())
+    for path in ("/swagger/", "/docs/", "/redoc/"):
+        r = c.get(path)
+        assert r.status_code == 200 and r.headers["content-type"].startswith("text/html")
+        assert not re.search(r"""(src|href)\s*=\s*["']?(https?:)?//""", r.text), path
+        assert "http://" not in r.text and "https://" not in r.text
+        assert "/swagger.json" in r.text
+    j = c.get("/docs.json").json()
+    assert "/api/v1/clusters/{name}/executions/" in j["paths"]
+    y = yaml.safe_load(c.get("/docs.yaml").text)
+    assert y["paths"].keys() == j["paths"].keys()
+    assert c.get("/swagger.json").json()["info"]["title"] == j["info"]["title"]
+
+
 def test_prometheus_metrics(client, control):
     from kubeoperator_amd.control.domain import deploy
     _register_hosts(client)

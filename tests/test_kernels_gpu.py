@@ -398,6 +398,40 @@ def test_flash_attention_bwd_dq_variants(variant, cfg, D, Hq, Hkv, S, causal):
         lib().flash_attn_set_dkdv_cfg(old_cfg)
 
 
+@pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 256, 4, 4), (2, 1024, 12, 12), (1, 512, 8, 2), (2, 768, 6, 3)])
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_attention_bwd_d64_two_wave(B, S, Hq, Hkv, causal):
+    """The D = 64 dK/dV kernel with two waves per SIMD (cfg 68, csrc/flash_bwd_d64.hip) against the fp32 autograd
+    reference -- direct bf16 dK / dV (Hq == Hkv) and the fp32-partial GQA path -- and against the one-wave kernel
+    (cfg 67): the same products in another summation order, so the gradients agree to bf16 rounding."""
+    from kubeoperator_amd.ops.functional import rope_attention
+    from kubeoperator_amd.ops.reference import attention_ref
+
+    D = 64
+    torch.manual_seed(B * S + Hq)
+    qkv0 = torch.randn(B * S, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
+    do = torch.randn(B * S, Hq * D, device=DEV, dtype=torch.bfloat16)
+    grads = {}
+    old_cfg = lib().flash_attn_set_dkdv_cfg(68)
+    try:
+        for cfg in (67, 68):
+            lib().flash_attn_set_dkdv_cfg(cfg)
+            qkv = qkv0.clone().requires_grad_(True)
+            o = rope_attention(qkv, None, None, B, S, Hq, Hkv, D, causal=causal, use_rope=False)
+            (o.float() * do.float()).sum().backward()
+            grads[cfg] = qkv.grad.float()
+    finally:
+        lib().flash_attn_set_dkdv_cfg(old_cfg)
+    x = qkv0.float().requires_grad_(True)
+    a, c = Hq * D, (Hq + Hkv) * D
+    of, _ = attention_ref(x[:, :a], x[:, a:c], x[:, c:], B, S, Hq, Hkv, D, causal)
+    (of * do.float()).sum().backward()
+    assert torch.isfinite(grads[68]).all()
+    for lo, hi in ((0, a), (a, c), (c, x.shape[1])):
+        assert rel_err(grads[68][:, lo:hi], x.grad[:, lo:hi]) < 3e-2
+        assert rel_err(grads[68][:, lo:hi], grads[67][:, lo:hi]) < 1e-2
+
+
 @pytest.mark.parametrize("hpw", [2, 4, 8])
 @pytest.mark.parametrize("D,cfg,B,S,Hq,Hkv", [(128, 64, 1, 768, 8, 2), (128, 64, 2, 512, 8, 1), (128, 64, 1, 1024, 16, 2),
                                               (64, 640, 1, 512, 8, 1), (128, 67, 1, 768, 8, 2), (128, 67, 2, 512, 8, 1),

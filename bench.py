@@ -26,8 +26,9 @@ collective, plus its stalls on ZeRO-1 all-gather gates in the next forward -- CU
 its GPU's NUMA-local CPUs and sizes its thread pool to them, ``parallel/dist.py`` ``bind_rank_cpus``, with the reason
 of any fallback). ``ranks`` (N > 1): one record per rank -- its pinning, its exposed waits (``finish_wait_ms``: the
 compute stream's stall for the last gradient collective; ``gate_wait_ms``: its stalls on ZeRO-1 all-gather gates) and
-its bucket timeline (``parallel/ddp.py`` ``timeline_summary``: when the buckets' gradients were ready and their
-collectives done, relative to backward's last kernel).
+its bucket timeline (``parallel/ddp.py`` ``timeline_summary``: when the buckets' gradients were ready, relative to
+backward's last kernel, and each collective's duration from RCCL's own events -- no extra stream). ``streams``: the
+HIP streams the rank issues work on against ``GPU_MAX_HW_QUEUES``.
 """
 from __future__ import annotations
 
@@ -59,7 +60,7 @@ def _self_launch(n: int) -> int:
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL peer buffers)
     # an even share of the CPUs this job may use per rank (each rank re-sizes its pool to the CPUs it is pinned to,
     # parallel/dist.py bind_rank_cpus): a fixed count per rank oversubscribes a small CPU share N-fold
-    env["OMP_NUM_THREADS"] = str(max(1, len(os.sched_getaffinity(0)) // n))
+    env.setdefault("OMP_NUM_THREADS", str(max(1, len(os.sched_getaffinity(0)) // n)))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
     print(f"[bench] --gpus {n} without torchrun: launching {n} ranks ({' '.join(cmd[1:6])} ...)", file=sys.stderr,
@@ -118,6 +119,9 @@ def main() -> int:
         return _self_launch(args.gpus)
     # a collective timeout tears the process group down and aborts the rank (non-zero exit, torchrun stops the rest)
     os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    # RCCL's own start / end events per collective: the bucket timeline reads them (Work._get_duration) instead of
+    # a stream of its own waiting on every collective
+    os.environ.setdefault("TORCH_NCCL_ENABLE_TIMING", "1")
 
     import torch
 
@@ -193,6 +197,7 @@ def main() -> int:
                "buckets": timeline_summary(trainer.dp.timeline)}
         ranks = gather_objects(rec, info)
         trainer.dp.finish_waits = trainer.store.gate_waits = trainer.dp.timeline = None
+    streams = stream_inventory(trainer, collectives_on(info)) if cuda else None
     comm_step = (trainer.dp.comm_bytes - comm0) // max(1, args.steps)
     gather_step = (trainer.dp.gather_bytes - gather0) // max(1, args.steps)
     gemm_tuning.finish(tuning, info.rank)
@@ -250,6 +255,7 @@ def main() -> int:
             "param_gather_bytes_per_step": int(gather_step),
             "exposed_comm_ms": round(exposed_ms, 3) if exposed_ms is not None else None,
             "cpu_affinity_rank0": affinity,
+            "streams": streams,
             "ranks": ranks,
             "runtime": runtime_env(),
         }
@@ -259,6 +265,25 @@ def main() -> int:
         torch.save(torch.cat([p.detach().reshape(-1).float().cpu() for _, p in trainer.store.named_params()]), dump)
     shutdown(info)
     return 0
+
+
+def stream_inventory(trainer, rccl: bool) -> dict:
+    """The HIP streams this rank issues work on, against the hardware queues a process gets (GPU_MAX_HW_QUEUES,
+    HIP's default 4): more streams than queues share queues, and work queued behind another stream's barrier
+    packets then waits for it. Warns on stderr when they do not fit."""
+    names = ["compute"]
+    if getattr(trainer.opt, "overlap", False):
+        names.append("optimizer")
+    if trainer.store.wgrad_stream:
+        names.append("wgrad")
+    if rccl:
+        names.append("rccl")
+    queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    fits = len(names) <= queues
+    if not fits:
+        print(f"[bench] warning: {len(names)} streams ({', '.join(names)}) > GPU_MAX_HW_QUEUES={queues}",
+              file=sys.stderr, flush=True)
+    return {"in_use": names, "hw_queues": queues, "fits": fits}
 
 
 def _dist_world() -> int:

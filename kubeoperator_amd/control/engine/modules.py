@@ -17,6 +17,7 @@ import shlex
 import time
 from dataclasses import dataclass, field
 
+from . import filecheck
 from .templating import render_text
 from .transport import CmdResult, FakeTransport, HostConn, Transport
 
@@ -122,6 +123,7 @@ def m_copy(ctx: ModuleContext, a: dict) -> dict:
         data = a["content"] if isinstance(a["content"], bytes) else str(a["content"]).encode()
         if dest.endswith("/"):
             raise ModuleError("copy with content needs a file dest")
+        _check_rendered(dest, data, a)
         return {"changed": _write_if_changed(ctx, dest, data, a, a.get("backup", False)), "dest": dest}
     src = str(a["src"])
     if a.get("remote_src"):
@@ -152,7 +154,18 @@ def m_template(ctx: ModuleContext, a: dict) -> dict:
     dest = str(a["dest"])
     if dest.endswith("/"):
         dest = os.path.join(dest, os.path.basename(local)[:-3] if local.endswith(".j2") else os.path.basename(local))
+    _check_rendered(dest, text.encode(), a)
     return {"changed": _write_if_changed(ctx, dest, text.encode(), a, a.get("backup", False)), "dest": dest}
+
+
+def _check_rendered(dest: str, data: bytes, a: dict) -> None:
+    """Parse a rendered file by type before it leaves the control node (engine/filecheck.py)."""
+    if a.get("validate", True) is False:
+        return
+    try:
+        filecheck.check(dest, data)
+    except filecheck.FileCheckError as e:
+        raise ModuleError(f"rendered file does not parse: {e}") from None
 
 
 def m_file(ctx: ModuleContext, a: dict) -> dict:

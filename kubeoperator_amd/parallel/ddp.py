@@ -55,11 +55,13 @@ class DataParallel:
         self.comm_bytes = 0  # gradient bytes handed to collectives (per rank, cumulative)
         self.gather_bytes = 0  # ZeRO-1 all-gather output bytes (per rank, cumulative)
         self.finish_waits: list | None = None  # (event, event) around finish_grads (exposed comm timing)
-        # bench: per optimizer step, every bucket's (index, grads-ready event, collective-done event) and backward's
-        # end, CUDA-event timed without host synchronisation (``timeline_summary`` turns them into a per-rank record)
+        # bench: per optimizer step, every bucket's (index, grads-ready event on the compute stream, collective Work)
+        # and backward's end. Passive: no stream of its own and no wait on the collective -- RCCL's own start / end
+        # events (TORCH_NCCL_ENABLE_TIMING=1) give each collective's duration after the timed region
+        # (``timeline_summary``). (An extra stream blocking on every collective could share a hardware queue with
+        # the compute stream under GPU_MAX_HW_QUEUES=4 and hold backward kernels behind it.)
         self.timeline: list | None = None
         self._tl_cur: list = []
-        self._tl_stream = None
         store.on_ready = self._on_ready
         self.overlapped = False  # set once the optimizer publishes ZeRO-1 gathers itself
         # one-rank RCCL self-test (parallel.dist.rccl_selftest): world-1 buckets still go through the collectives
@@ -92,15 +94,7 @@ class DataParallel:
             a, e = b.piece(rank, world)
             self._works.append(dist.reduce_scatter_tensor(self.store.grads[a:e], g, group=group, async_op=True))
         if timed:
-            # the collective's completion, seen from an otherwise idle stream: wait() under it makes THAT stream (not
-            # the compute stream) wait for RCCL, and the event behind it fires when the collective is done
-            if self._tl_stream is None:
-                self._tl_stream = torch.cuda.Stream(device=g.device)
-            done = torch.cuda.Event(enable_timing=True)
-            with torch.cuda.stream(self._tl_stream):
-                self._works[-1].wait()
-                done.record()
-            self._tl_cur.append((b.index, ready, done))
+            self._tl_cur.append((b.index, ready, self._works[-1]))
 
     def finish_grads(self) -> None:
         """Make the current (compute) stream wait for every outstanding gradient collective. With
@@ -198,12 +192,24 @@ class DataParallel:
         self._gather_works.clear()
 
 
+def _duration_ms(work) -> float | None:
+    """A finished collective's GPU time from RCCL's start / end events (``TORCH_NCCL_ENABLE_TIMING=1``), else None."""
+    try:
+        d = work._get_duration()
+    except (RuntimeError, AttributeError, ValueError):
+        return None
+    return float(d) if d is not None and d >= 0 else None
+
+
 def timeline_summary(steps: list[dict]) -> dict | None:
     """Per-rank gradient-collective timeline (bench JSON), from ``DataParallel.timeline`` after a synchronize.
 
     Times are ms relative to backward's last kernel on the compute stream (negative: before it), medians over the
-    timed steps: when the first / last bucket's gradients were ready, when the first / last collective completed,
-    and the span the collectives were in flight. ``last_done_ms`` > 0 is communication exposed after backward."""
+    timed steps. Measured: when each bucket's gradients were ready (compute-stream events) and each collective's own
+    duration (RCCL's events, ``Work._get_duration``). Derived: the collectives run one after another on RCCL's
+    stream, so collective i starts at max(its bucket ready, collective i-1 done) and is done ``duration`` later --
+    ``last_done_ms`` > 0 is communication exposed after backward, ``comm_ms`` the summed collective time. Without
+    RCCL timing (durations unavailable) only the ready times are reported."""
     rows = []
     for st in steps:
         bk = st["buckets"]
@@ -213,9 +219,16 @@ def timeline_summary(steps: list[dict]) -> dict | None:
         t = lambda ev: ref.elapsed_time(ev)  # noqa: E731
         end = t(st["bwd_end"])
         ready = [t(r) - end for _, r, _ in bk]
-        done = [t(d) - end for _, _, d in bk]
-        rows.append({"n_buckets": len(bk), "first_ready_ms": min(ready), "last_ready_ms": max(ready),
-                     "first_done_ms": min(done), "last_done_ms": max(done), "in_flight_ms": max(done) - min(ready)})
+        row = {"n_buckets": len(bk), "first_ready_ms": min(ready), "last_ready_ms": max(ready)}
+        durs = [_duration_ms(w) for _, _, w in bk]
+        if all(d is not None for d in durs):
+            done, prev = [], float("-inf")
+            for rd, d in zip(ready, durs):
+                prev = max(rd, prev) + d
+                done.append(prev)
+            row.update({"first_done_ms": min(done), "last_done_ms": max(done), "in_flight_ms": max(done) - min(ready),
+                        "comm_ms": sum(durs), "max_collective_ms": max(durs)})
+        rows.append(row)
     return summarize_rows(rows)
 
 

@@ -147,7 +147,7 @@ def _fmt_cpus(want: list[int]) -> str:
 def bind_rank_cpus(info: DistInfo) -> dict | None:
     """Pin this rank to the CPUs next to its GPU (``plan_rank_cpus``) and size torch's intra-op thread pool to them
     (``rank_threads``). Multi-rank GPU jobs only (the one-GPU headline runs unpinned); ``KOP_CPU_AFFINITY=0`` turns
-    the pinning off (the thread count is still set). Returns what was done and why, for the bench JSON:
+    the pinning off (and with OMP_NUM_THREADS set, leaves the pool alone); ``KOP_RANK_THREADS`` forces the count. Returns what was done and why, for the bench JSON:
     {"rank", "gpu", "numa_node", "cpus", "ncpus", "allowed", "threads", "reason"} (None: one rank / CPU)."""
     if info.device.type != "cuda" or info.world <= 1:
         return None
@@ -167,7 +167,14 @@ def bind_rank_cpus(info: DistInfo) -> dict | None:
             rec["cpus"], rec["ncpus"] = _fmt_cpus(want), len(want)
         except (OSError, ValueError, RuntimeError, KeyError) as e:
             rec["reason"] = f"unpinned: {type(e).__name__}: {e}"[:160]
-    rec["threads"] = rank_threads(rec["ncpus"], len(allowed), nloc)
+    forced = os.environ.get("KOP_RANK_THREADS")
+    if forced:  # the operator's choice
+        rec["threads"] = max(1, int(forced))
+    elif os.environ.get("KOP_CPU_AFFINITY", "1") == "0" and os.environ.get("OMP_NUM_THREADS"):
+        rec["threads"] = torch.get_num_threads()  # unpinned: the pool stays as OMP_NUM_THREADS made it
+        return rec
+    else:
+        rec["threads"] = rank_threads(rec["ncpus"], len(allowed), nloc)
     torch.set_num_threads(rec["threads"])
     os.environ["OMP_NUM_THREADS"] = str(rec["threads"])  # for anything this rank starts later
     return rec

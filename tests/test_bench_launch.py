@@ -176,15 +176,19 @@ def test_rank_threads_never_oversubscribe(monkeypatch):
     assert rank_threads(0, 16, 8) == 2  # unpinned: an even share of the allowed CPUs, not OMP's 16 each
     assert rank_threads(None, 4, 8) == 1
 
-    # the self-launch hands each child rank an even share of this process's CPUs
+    # the self-launch hands each child rank an even share of this process's CPUs unless the operator set a count
+    # (each rank re-sizes its pool in bind_rank_cpus anyway)
     import bench
 
     seen = {}
     monkeypatch.setattr(os, "sched_getaffinity", lambda pid: set(range(16)))
     monkeypatch.setattr(subprocess, "call", lambda cmd, env=None: seen.update(env=env) or 0)
-    monkeypatch.setenv("OMP_NUM_THREADS", "16")
+    monkeypatch.delenv("OMP_NUM_THREADS", raising=False)
     assert bench._self_launch(8) == 0
     assert seen["env"]["OMP_NUM_THREADS"] == "2"
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    assert bench._self_launch(8) == 0
+    assert seen["env"]["OMP_NUM_THREADS"] == "3"
 
 
 def test_bucket_timeline_summary_is_the_median_over_steps():
@@ -196,3 +200,59 @@ def test_bucket_timeline_summary_is_the_median_over_steps():
     assert s == {"n_buckets": 3, "first_ready_ms": -41.0, "last_ready_ms": -1.0, "first_done_ms": -30.0,
                  "last_done_ms": 3.0, "in_flight_ms": 42.0, "steps": 3}
     assert summarize_rows([]) is None
+
+
+def test_bucket_timeline_is_passive_and_uses_rccl_durations():
+    """The timeline records compute-stream ready events and RCCL's own per-collective durations (Work._get_duration,
+    TORCH_NCCL_ENABLE_TIMING=1): collective i runs from max(ready_i, done_{i-1}) for its duration. No stream of
+    its own (ddp.DataParallel has no timeline stream any more)."""
+    from kubeoperator_amd.parallel import ddp
+
+    class Ev:
+        def __init__(self, t):
+            self.t = t
+
+        def elapsed_time(self, other):
+            return other.t - self.t
+
+    class Work:
+        def __init__(self, d):
+            self.d = d
+
+        def _get_duration(self):
+            if self.d is None:
+                raise RuntimeError("timing not enabled")
+            return self.d
+
+    # backward ends at t = 10; buckets ready at 2, 5, 9; collectives of 4, 1, 3 ms
+    step = {"bwd_end": Ev(10.0), "buckets": [(0, Ev(2.0), Work(4.0)), (1, Ev(5.0), Work(1.0)), (2, Ev(9.0), Work(3.0))]}
+    s = ddp.timeline_summary([step, step, step])
+    assert s["n_buckets"] == 3 and s["steps"] == 3
+    assert s["first_ready_ms"] == -8.0 and s["last_ready_ms"] == -1.0
+    # done: 2+4 = 6, max(5, 6)+1 = 7, max(9, 7)+3 = 12 -> relative to 10: -4, -3, +2
+    assert s["first_done_ms"] == -4.0 and s["last_done_ms"] == 2.0 and s["comm_ms"] == 8.0
+    assert s["in_flight_ms"] == 10.0 and s["max_collective_ms"] == 4.0
+    # without RCCL timing: ready times only
+    step2 = {"bwd_end": Ev(10.0), "buckets": [(0, Ev(2.0), Work(None))]}
+    s2 = ddp.timeline_summary([step2])
+    assert "last_done_ms" not in s2 and s2["last_ready_ms"] == -8.0
+    import inspect
+
+    assert "Stream(" not in inspect.getsource(ddp)
+
+
+def test_stream_inventory_against_hw_queues(monkeypatch):
+    import bench
+
+    class T:
+        class opt:
+            overlap = True
+
+        class store:
+            wgrad_stream = True
+
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    inv = bench.stream_inventory(T, rccl=True)
+    assert inv == {"in_use": ["compute", "optimizer", "wgrad", "rccl"], "hw_queues": 4, "fits": True}
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "2")
+    assert bench.stream_inventory(T, rccl=True)["fits"] is False

@@ -86,16 +86,23 @@ __global__ void __launch_bounds__(NT) ce_fwd_kernel(bf16_t* __restrict__ logits,
   // pass 2: (softmax - onehot) * scale = exp2(f log2 e - lse log2 e + log2 sc) for every logit (the scale folded into
   // the exponent: one FMA + one exponential + the pack), then the target's own element is rewritten once below
   // instead of an index compare per logit
-  const float b2 = sc > 0.f ? (__log2f(sc) - lse * L2E) : -INFINITY;
+  // |sc| goes into the exponent, its sign is applied after (a negative grad_multiplier flips every element; the sign
+  // branch is uniform, so the common sc > 0 loop carries no extra multiply)
+  const float b2 = sc != 0.f ? (__log2f(fabsf(sc)) - lse * L2E) : -INFINITY;
+  const float sg = sc < 0.f ? -1.f : 1.f;
   u32x4* xw = reinterpret_cast<u32x4*>(x);
   for (int c = threadIdx.x; c < V8; c += NT) {
     float f[8];
     unpack8(xw[c], f);
 #pragma unroll
     for (int i = 0; i < 8; ++i) f[i] = __builtin_amdgcn_exp2f(fmaf(f[i], L2E, b2));
+    if (sc < 0.f) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) f[i] = -f[i];
+    }
     xw[c] = pack8(f);
   }
-  for (int i = V8 * 8 + threadIdx.x; i < V; i += NT) x[i] = f2bf(__builtin_amdgcn_exp2f(fmaf(bf2f(x[i]), L2E, b2)));
+  for (int i = V8 * 8 + threadIdx.x; i < V; i += NT) x[i] = f2bf(sg * __builtin_amdgcn_exp2f(fmaf(bf2f(x[i]), L2E, b2)));
   if (valid) {
     __syncthreads();  // the target's element has been written by its owner above
     if (threadIdx.x == 0) x[t] = f2bf((__expf(xt - lse) - 1.f) * sc);
@@ -154,7 +161,7 @@ __global__ void __launch_bounds__(NT) ce_fwd_reg_kernel(bf16_t* __restrict__ log
   }
   if (!write_grad) return;
   const float sc = valid ? scale_p[0] : 0.f;
-  const float b2 = sc > 0.f ? (__log2f(sc) - lse * L2E) : -INFINITY;
+  const float b2 = sc != 0.f ? (__log2f(fabsf(sc)) - lse * L2E) : -INFINITY;  // sign applied below (two-pass kernel)
   __syncthreads();  // x[t] read above before any thread overwrites it
 #pragma unroll
   for (int j = 0; j < CPT; ++j) {
@@ -164,6 +171,10 @@ __global__ void __launch_bounds__(NT) ce_fwd_reg_kernel(bf16_t* __restrict__ log
     unpack8(w[j], f);
 #pragma unroll
     for (int i = 0; i < 8; ++i) f[i] = __builtin_amdgcn_exp2f(fmaf(f[i], L2E, b2));
+    if (sc < 0.f) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) f[i] = -f[i];
+    }
     xw[c] = pack8(f);
   }
   if (valid) {

@@ -12,7 +12,7 @@
 //
 // Pass 1: grid (splits, B * Hkv), 256 threads. A workgroup owns CH = 128 keys of one (sequence, KV head).
 // Default: decode_attn_mfma_kernel (both products on 16x16x32 MFMAs, G heads as padded columns; below). The VALU
-// form (KOP_DECODE_ATTN=valu; KOP_DECODE_CH=256: 256 keys per workgroup):
+// form (KOP_DECODE_ATTN=valu):
 //   thread t = (key group kg = t / 16, segment sg = t % 16): the 16 threads of a key group read one 256-byte
 //   K row (D = 128) as 16 x 16 B -- a wave loads 4 whole rows per instruction -- and each keeps G partial dot
 //   products of its 8 dims, summed over the 16 lanes with 4 butterfly shuffles. Scores (already scaled by
@@ -431,13 +431,7 @@ __global__ void __launch_bounds__(64) decode_attn_combine_kernel(const float* __
   else op[0] = f2bf(a[0] * inv);
 }
 
-static int chunk_keys() {
-  static const int ch = [] {
-    const char* e = getenv("KOP_DECODE_CH");  // 128 (default): -2 % per step at batch 128 vs 256, same at 64
-    return (e && atoi(e) == 256) ? 256 : 128;
-  }();
-  return ch;
-}
+static constexpr int chunk_keys() { return 128; }  // keys per pass-1 workgroup (256 measured -2 % at batch 128)
 
 // ---------------------------------------------------------------------------------------------------------
 // Decode-step append: RoPE at each sequence's position on its new Q and K heads (in place in the fused QKV row)
@@ -522,14 +516,11 @@ int decode_attn_set_mfma(int on) {
 template <int D, int G>
 static void launch_split(const bf16_t* q, int64_t qs, const bf16_t* kc, const bf16_t* vc, const int* lens, int B,
                          int Smax, int Hkv, float sl2, float* po, float* pml, int nsplit, hipStream_t stream) {
-  if (chunk_keys() == 128 && decode_mfma())
+  if (decode_mfma())
     decode_attn_mfma_kernel<D, G><<<dim3(nsplit, B * Hkv), kThreads, 0, stream>>>(q, qs, kc, vc, lens, Smax, Hkv, sl2,
                                                                                  po, pml, nsplit);
-  else if (chunk_keys() == 128)
-    decode_attn_split_kernel<D, G, 128><<<dim3(nsplit, B * Hkv), kThreads, 0, stream>>>(q, qs, kc, vc, lens, Smax, Hkv,
-                                                                                       sl2, po, pml, nsplit);
   else
-    decode_attn_split_kernel<D, G, 256><<<dim3(nsplit, B * Hkv), kThreads, 0, stream>>>(q, qs, kc, vc, lens, Smax, Hkv,
+    decode_attn_split_kernel<D, G, 128><<<dim3(nsplit, B * Hkv), kThreads, 0, stream>>>(q, qs, kc, vc, lens, Smax, Hkv,
                                                                                        sl2, po, pml, nsplit);
 }
 

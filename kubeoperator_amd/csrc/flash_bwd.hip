@@ -976,8 +976,8 @@ static int g_dkdv_cfg = -1;  // -1: read KOP_DKDV_CFG on first use
 static int dkdv_cfg() {
   if (g_dkdv_cfg < 0) {
     // 67 (default): one wave per SIMD, 64 keys per wave, key-major dS tiles stored from registers (D = 128); 64: the
-    // same with the LDS-staged wave-block dS; 66: LDS-staged row-major dS; 42: two waves per SIMD (every D); 83 / 82:
-    // 8-wave workgroups with a 3- / 2-deep stage ring (D = 128). 67 vs 64: causal backward 1.731 / 1.721 ms vs
+    // same with the LDS-staged wave-block dS; 66: LDS-staged row-major dS; 42: two waves per SIMD, 32 keys per wave, 4-wave
+    // workgroups (every D); 68: the D = 64 two-waves-per-SIMD kernel of flash_bwd_d64.hip. 67 vs 64: causal backward 1.731 / 1.721 ms vs
     // 1.778 / 1.790 ms at the Llama-3-8B shape, same box (profiles/r4_dkdv_kmaj_ab.jsonl)
     const char* e = getenv("KOP_DKDV_CFG");
     g_dkdv_cfg = e ? atoi(e) : 67;
@@ -1051,18 +1051,6 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
       np = flash_attn_bwd_dkdv64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, D, qs, ks, vs,
                                  dos, dks, dvs, scale, cflag, !kmaj, blk, stream);
       done = true;
-    }
-    if constexpr (D == 128) {
-      // 8-wave workgroups (>= 8 1-KiB pieces per 32-row x 256-B Q / dO tile) with a 3- or 2-deep stage ring
-      if (!done && cfg == 83 && S % 256 == 0) {
-        launch_dkdv_ds<D, 8, 3>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs,
-                                dos, dks, dvs, scale, cflag, stream);
-        done = true;
-      } else if (!done && cfg == 82 && S % 256 == 0) {
-        launch_dkdv_ds<D, 8, 2>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs,
-                                dos, dks, dvs, scale, cflag, stream);
-        done = true;
-      }
     }
     if (!done)
       launch_dkdv_ds<D, NW, 2>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs,

@@ -599,14 +599,17 @@ static int dkdv64_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, cons
   constexpr int NS = 3;
   const size_t lds = 256 * (D * 2) + NS * (2 * 32 * (D * 2) + 1024) + 4 * 4096;
   const int grp = Hq / Hkv;
+#ifdef KOP_ABLATIONS
+  // timing ablations of the stage (DIAG bits above; WRONG dK / dV / dS except 16 / 64 / 128): compiled only into the
+  // probe build of tools/ (-DKOP_ABLATIONS), never into the shipped extension
   static const int diag = [] {
     const char* e = getenv("KOP_DKDV64_DIAG");
     return e ? atoi(e) : 0;
   }();
+#endif
   // one instantiation per (DIRECT, QM, DIAG, BLK, REV, HPW) actually launched; the dynamic-LDS attribute is set on
   // first use. Returns the number of partials per GQA group the finalize pass must sum (0: dK / dV written).
 #define KOP_LAUNCH(DIR, QMV, DG, BL) KOP_LAUNCH_R(DIR, QMV, DG, BL, true, 1)
-#define KOP_LAUNCH_FWD(DIR, QMV, DG, BL) KOP_LAUNCH_R(DIR, QMV, DG, BL, false, 1)
 #define KOP_LAUNCH_R(DIR, QMV, DG, BL, RV, HP)                                                                         \
   do {                                                                                                             \
     static bool attr = false;                                                                                      \
@@ -625,10 +628,7 @@ static int dkdv64_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, cons
           q, k, v, dout, nlse, ndelta, dk_part, dv_part, ds, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal, 0, 0);  \
     return (DIR) ? 0 : grp / (HP);                                                                                 \
   } while (0)
-  static const bool rev = [] {
-    const char* e = getenv("KOP_DKDV_REV");  // reversed stage sweep (default on); 0: forward order
-    return e ? atoi(e) != 0 : true;
-  }();
+#ifdef KOP_ABLATIONS
   if (diag != 0 && Hq != Hkv && qm && ds != nullptr) {
     switch (diag) {
       case 1: KOP_LAUNCH(false, true, 1, false);
@@ -641,15 +641,13 @@ static int dkdv64_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, cons
       default: break;
     }
   }
+#endif
   if (ds == nullptr) {  // no dS at all (dQ recomputes it): the store-free build
     if (Hq == Hkv) KOP_LAUNCH(true, true, 1, false);
     else KOP_LAUNCH(false, true, 1, false);
   }
-  if (!rev && Hq != Hkv && qm) {  // forward stage order (A/B)
-    if (blk_layout) KOP_LAUNCH_FWD(false, true, 0, true);
-    else KOP_LAUNCH_FWD(false, true, 0, false);
-  }
   if (Hq == Hkv) {
+#ifdef KOP_ABLATIONS
     if (diag != 0 && blk_layout && !qm) {  // timing ablations of the KT build (wrong results except 0)
       switch (diag) {
         case 1: KOP_LAUNCH(true, false, 1, true);
@@ -661,16 +659,19 @@ static int dkdv64_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, cons
         default: break;
       }
     }
+#endif
     if (blk_layout && !qm) KOP_LAUNCH(true, false, 0, true);  // KT tiles
     if (blk_layout) KOP_LAUNCH(true, true, 0, true);
     else KOP_LAUNCH(true, true, 0, false);
   }
   const int hpw = pick_hpw(B, S, Hq, Hkv, causal != 0);
   if (blk_layout && !qm) {  // KT tiles: dS stored straight from the accumulators
+#ifdef KOP_ABLATIONS
     if (diag == 1 && hpw == 2 && grp != 2) KOP_LAUNCH_R(false, false, 1, true, true, 2);  // ablation: no dS stores
     if (diag == 64 && hpw == 2 && grp != 2) KOP_LAUNCH_R(false, false, 64, true, true, 2);  // sc1 dS stores
     if (diag == 128 && hpw == 2 && grp != 2) KOP_LAUNCH_R(false, false, 128, true, true, 2);  // plain dS stores
     if (diag == 256 && hpw == 2 && grp != 2) KOP_LAUNCH_R(false, false, 256, true, true, 2);  // stores to one tile
+#endif
     switch (hpw) {
       case 2: if (grp == 2) KOP_LAUNCH_R(true, false, 0, true, true, 2); else KOP_LAUNCH_R(false, false, 0, true, true, 2);
       case 4: if (grp == 4) KOP_LAUNCH_R(true, false, 0, true, true, 4); else KOP_LAUNCH_R(false, false, 0, true, true, 4);
@@ -688,7 +689,6 @@ static int dkdv64_launch(const bf16_t* q, const bf16_t* k, const bf16_t* v, cons
   }
   KOP_LAUNCH(false, true, 0, false);
 #undef KOP_LAUNCH
-#undef KOP_LAUNCH_FWD
 #undef KOP_LAUNCH_R
 }
 

@@ -295,21 +295,9 @@ int flash_attn_fwd16(const bf16_t* q, const bf16_t* k, const bf16_t* v, bf16_t* 
                      int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, float sl2, bool causal,
                      hipStream_t stream, bf16_t* ot) {
   if (S % 256 != 0 || Hq % Hkv != 0 || (D != 64 && D != 128)) return -1;
-  static const int vd = [] {
-    const char* e = getenv("KOP_FWD16_VD");
-    const int x = e ? atoi(e) : 2;  // 1-3 within 1 % of each other (profiles/r5_fwd16_vdepth_ab.jsonl)
-    return x < 1 ? 1 : (x > 3 ? 3 : x);
-  }();
-#define KOP_F16(DV)                                                                                              \
-  if (vd == 1) launch_fwd16<DV, 1>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream, ot);      \
-  else if (vd == 2) launch_fwd16<DV, 2>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream, ot); \
-  else launch_fwd16<DV, 3>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream, ot);
-  if (D == 128) {
-    KOP_F16(128)
-  } else {
-    KOP_F16(64)
-  }
-#undef KOP_F16
+  // V^T read-ahead depth 2 (depths 1-3 measured within 1 % of each other: profiles/r5_fwd16_vdepth_ab.jsonl)
+  if (D == 128) launch_fwd16<128, 2>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream, ot);
+  else launch_fwd16<64, 2>(q, k, v, o, lse, B, S, Hq, Hkv, qs, ks, vs, os, sl2, causal, stream, ot);
   return 0;
 }
 

@@ -64,6 +64,10 @@ FILE_FLAGS = {"flash_bwd_w1.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=true"],
               "flash_fwd4.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=true", "-fno-slp-vectorize", "-fno-honor-nans"]}
 
 
+# probe builds only (tools/build_ab.py --ablations): never set for the shipped extension
+EXTRA_HIPFLAGS: list[str] = []
+
+
 def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -> str:
     """Compile every kernel for gfx950 and link ``_C.so``; returns its path."""
     os.makedirs(BUILD_DIR, exist_ok=True)
@@ -79,7 +83,8 @@ def build(verbose: bool = False, jobs: int | None = None, force: bool = False) -
         objs.append(obj)
         if force or _needs(obj, src, hdr):
             jobs_list.append([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics",
-                              abi, *FILE_FLAGS.get(os.path.basename(src), []), "-I", CSRC, "-c", src, "-o", obj])
+                              abi, *FILE_FLAGS.get(os.path.basename(src), []), *EXTRA_HIPFLAGS, "-I", CSRC, "-c", src,
+                              "-o", obj])
     bsrc = os.path.join(CSRC, "bindings.cpp")
     bobj = os.path.join(BUILD_DIR, "bindings.cpp.o")
     objs.append(bobj)

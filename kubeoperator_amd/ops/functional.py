@@ -495,9 +495,12 @@ class _Norm(Function):
             # also write dx^T: the dY operand of the weight gradient of the projection that produced x
             dx, dxt = lib.rms_norm_bwd_t(dy, s, w, rstd, dres, dw_buf, acc and not staged)
             ctx.box.put(dx, dxt)
-        elif _NORM_SIDE and mg_w is not None and not staged and _side_active(w):
+        elif (_NORM_SIDE and mg_w is not None and not staged and _side_active(w)
+              and (not ctx.layernorm or db_buf is mg_b)):
             # the weight / bias gradient fold (two column reductions) goes to the weight-gradient stream: it is not on
-            # the data-gradient chain, and there it no longer waits for CUs behind that stream's GEMMs
+            # the data-gradient chain, and there it no longer waits for CUs behind that stream's GEMMs. Only when both
+            # outputs are the parameters' main_grad views: a temporary bias buffer (frozen bias, no main_grad) would be
+            # freed to the compute stream's allocator while the side-stream kernel still writes it
             dx, part = lib.norm_bwd_parts(dy, s, w, rstd, mean, dres, ctx.layernorm)
             _side_launch(w, lambda: lib.norm_bwd_reduce_(part, dw_buf, db_buf, ctx.layernorm, acc), part)
         else:

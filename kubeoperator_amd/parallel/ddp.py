@@ -63,6 +63,7 @@ class DataParallel:
         self.timeline: list | None = None
         self._tl_cur: list = []
         store.on_ready = self._on_ready
+        store.collectives_live = lambda: self.sync and (self.world > 1 or self.force or self.sp)
         self.overlapped = False  # set once the optimizer publishes ZeRO-1 gathers itself
         # one-rank RCCL self-test (parallel.dist.rccl_selftest): world-1 buckets still go through the collectives
         self.force = info.world == 1 and collectives_on(info)

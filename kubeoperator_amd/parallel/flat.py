@@ -152,6 +152,8 @@ class FlatParamStore:
         self._bucket_of: dict[int, Bucket] = {}
         self._param_by_name: dict[str, nn.Parameter] = {}
         self.on_ready = None  # callable(Bucket)
+        # True while readiness launches gradient collectives this micro-batch (DataParallel sets it); defer() refuses then
+        self.collectives_live = lambda: False
         self.gates: dict[int, object] = {}  # bucket index -> torch.cuda.Event | collective work
         self.use_order: list[int] = []  # bucket indices in the order the forward pass first reads them
         self._used: set[int] = set()
@@ -268,7 +270,15 @@ class FlatParamStore:
         held.append((ev, tuple(tensors)))
 
     def defer(self, launch) -> None:
-        """Queue a side-stream gradient launch for ``run_deferred`` (ops.functional._sink(defer=True))."""
+        """Queue a side-stream gradient launch for ``run_deferred`` (ops.functional._sink(defer=True)).
+
+        ``_sink`` marks the parameter ready BEFORE the deferred launch writes its gradient, which is only sound while
+        no bucket collective fires on readiness this micro-batch (data parallelism reduces buckets on the last
+        micro-batch only, where the trainer turns ``defer_ok`` off). Enforced here, not assumed."""
+        if self.collectives_live():
+            raise RuntimeError("weight-gradient launch deferred while bucket collectives are live: a bucket would be "
+                               "reduced before its deferred gradient is written (defer_ok must be off on the "
+                               "micro-batch whose backward reduces)")
         self._deferred.append(launch)
 
     def run_deferred(self) -> None:

@@ -256,3 +256,22 @@ def test_stream_inventory_against_hw_queues(monkeypatch):
     assert inv == {"in_use": ["compute", "optimizer", "wgrad", "rccl"], "hw_queues": 4, "fits": True}
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "2")
     assert bench.stream_inventory(T, rccl=True)["fits"] is False
+
+
+def test_deferred_weight_gradient_refused_while_collectives_live():
+    """_sink(defer=True) marks a parameter ready before its deferred gradient launch; that is only sound
+    while readiness launches no bucket collective. The flat store refuses a deferral on a micro-batch whose backward
+    reduces (dp.sync on, collectives on) instead of relying on the trainer's defer_ok wiring."""
+    import pytest
+
+    from kubeoperator_amd.parallel.dist import DistInfo
+    from kubeoperator_amd.train import TrainConfig, Trainer
+
+    tr = Trainer(TrainConfig(model="tiny_llama", micro_batch=1, seq_len=32), DistInfo())
+    tr.dp.sync = False
+    tr.store.defer(lambda: None)
+    tr.store.run_deferred()
+    tr.dp.force = True  # as the one-rank RCCL self-test: buckets go through collectives
+    tr.dp.sync = True
+    with pytest.raises(RuntimeError, match="collectives are live"):
+        tr.store.defer(lambda: None)

@@ -293,10 +293,10 @@ def test_role_default_referencing_other_vars_is_expanded(tmp_path):
         max_pods: "{{ MAX_PODS | default(110) }}"
         opts: {dir: "{{ state }}", pods: "{{ max_pods }}"}
     """))
-    (role / "templates" / "c.toml.j2").write_text("root = \"{{ root }}\"\nstate = \"{{ state }}\"\n"
+    (role / "templates" / "c.conf.j2").write_text("root = \"{{ root }}\"\nstate = \"{{ state }}\"\n"
                                                   "pods = {{ max_pods | int + 1 }}\ndir = {{ opts.dir }}\n")
     (role / "tasks" / "main.yml").write_text(textwrap.dedent("""
-        - template: src=c.toml.j2 dest=/etc/c.toml
+        - template: src=c.conf.j2 dest=/etc/c.conf
         - shell: "mkdir -p {{ root }} && echo {{ hostvars[inventory_hostname]['hv'] }}"
     """))
     inv = _inv()
@@ -307,7 +307,7 @@ def test_role_default_referencing_other_vars_is_expanded(tmp_path):
       roles: [rt]
     """, inv=inv, roles_path=[str(tmp_path / "roles")], extra_vars={"STORAGE_DIR": "/data/ctr", "MAX_PODS": 200})
     assert res["summary"]["success"], res["summary"]
-    assert t.fs["w1"]["/etc/c.toml"] == b'root = "/data/ctr"\nstate = "/data/ctr/state"\npods = 201\n' \
+    assert t.fs["w1"]["/etc/c.conf"] == b'root = "/data/ctr"\nstate = "/data/ctr/state"\npods = 201\n' \
                                         b'dir = /data/ctr/state\n'
     assert "mkdir -p /data/ctr && echo all-/data/ctr" in t.commands("w1")
 

@@ -166,6 +166,33 @@ def test_cross_entropy_lmhead(V):
     assert rel_err(w.grad, wf.grad) < 3e-2
 
 
+@pytest.mark.parametrize("V", [50304, 128256])
+@pytest.mark.parametrize("mult", [2.0, -1.5, 0.0])
+def test_cross_entropy_grad_multiplier_sign(V, mult):
+    """The gradient the kernel writes in place is (softmax - onehot) * grad_multiplier / n_valid for ANY sign of the
+    multiplier (its magnitude is folded into the exponent, the sign applied separately)."""
+    torch.manual_seed(15)
+    T = 64
+    logits = (2 * torch.randn(T, V, device=DEV)).to(torch.bfloat16)
+    tgt = torch.randint(0, V, (T,), device=DEV)
+    tgt[::5] = -100
+    ref_in = logits.float()
+    x = logits.clone()
+    lib().cross_entropy_fwd_(x, tgt, -100, True, mult)
+    n = int((tgt != -100).sum())
+    p = torch.softmax(ref_in, -1)
+    oh = torch.zeros_like(p)
+    valid = tgt != -100
+    oh[valid.nonzero().squeeze(1), tgt[valid]] = 1.0
+    ref = (p - oh) * (mult / n)
+    ref[~valid] = 0.0
+    if mult == 0.0:
+        assert torch.count_nonzero(x[valid].float()) == 0
+    else:
+        assert rel_err(x[valid], ref[valid]) < 2e-2
+        assert (x[valid].float() * ref[valid]).sum() > 0  # same sign pattern as the reference
+
+
 def test_adamw_matches_reference():
     from kubeoperator_amd.ops.optim import FusedAdamW, Segment
 
@@ -219,10 +246,11 @@ def test_flash_attention_fwd(D, causal):
     check_against_bf16("o", o.reshape(-1, D), o_ref.reshape(-1, D), ob.reshape(-1, D))
 
 
-@pytest.mark.parametrize("variant", [-1, 10, 8, 9, 0, 16])
+@pytest.mark.parametrize("variant", [-1, 10, 8, 9, 0, 16, 12])
 def test_flash_attention_fwd_spiked_rescale(variant):
     """force the online-softmax rescale branch: a large score late in the key sweep (every forward kernel:
-    -1 the default, 8 / 9 / 10 the 8-wave kernel, 0 the 4-wave kernel, 16 the 16x16x32-MFMA kernel)."""
+    -1 the default, 8 / 9 / 10 the 8-wave kernel, 0 the 4-wave kernel, 16 the 16x16x32-MFMA kernel, 12 the
+    hand-scheduled one-wave-per-SIMD kernel of flash_fwd4.hip)."""
     from kubeoperator_amd.ops.functional import flash_attention
     from kubeoperator_amd.ops.reference import attention_ref
 
@@ -241,12 +269,12 @@ def test_flash_attention_fwd_spiked_rescale(variant):
         lib().flash_attn_set_fwd_variant(old)
 
 
-@pytest.mark.parametrize("variant,D", [(8, 128), (10, 128), (16, 128), (16, 64)])
+@pytest.mark.parametrize("variant,D", [(8, 128), (10, 128), (16, 128), (16, 64), (12, 128)])
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 512, 8, 2), (1, 1024, 4, 4), (2, 256, 6, 3)])
 @pytest.mark.parametrize("causal", [True, False])
 def test_flash_attention_fwd_variants_d128(variant, D, B, S, Hq, Hkv, causal):
-    """the 8-wave forward (scalar / packed FMA softmax; 16: on 16x16x32 MFMAs, also at D = 64) against the fp32
-    reference with GQA groups of 4, 1 and 2, with and without the O^T output (which must be the exact transpose of O)."""
+    """the 8-wave forward (scalar / packed FMA softmax; 16: on 16x16x32 MFMAs, also at D = 64; 12: the hand-scheduled
+    one-wave-per-SIMD kernel, flash_fwd4.hip) against the fp32 reference with GQA groups of 4, 1 and 2, with and without the O^T output (which must be the exact transpose of O)."""
     from kubeoperator_amd.ops.reference import attention_ref
 
     old = lib().flash_attn_set_fwd_variant(variant)
@@ -363,10 +391,11 @@ def test_weight_grad_tn_layout_matches_nt(layout, monkeypatch):
         assert rel_err(out, 2 * ref) < 1e-2
 
 
-@pytest.mark.parametrize("variant,cfg", [(10, 64), (10, 66), (10, 67), (10, 640), (10, 670), (10, 42), (9, 64), (9, 42),
-                                         (8, 42)],
+@pytest.mark.parametrize("variant,cfg", [(10, 64), (10, 66), (10, 67), (10, 640), (10, 670), (10, 42), (10, 68), (9, 64),
+                                         (9, 42), (8, 42), (0, 42)],
                          ids=["ds_blk-dkdv64", "ds-dkdv66", "ds_kmaj-dkdv67", "ds_blk-dkdv64_d64", "ds_kmaj-dkdv67_d64",
-                              "ds-dkdv42", "recompute9-dkdv64", "recompute9", "recompute8"])
+                              "ds-dkdv42", "ds_kmaj-dkdv68_d64", "recompute9-dkdv64", "recompute9", "recompute8",
+                              "recompute4w"])
 @pytest.mark.parametrize("D,Hq,Hkv,S", [(128, 8, 2, 512), (64, 4, 4, 256), (128, 4, 1, 768), (128, 8, 1, 256),
                                         (64, 8, 4, 512), (128, 4, 4, 512), (128, 6, 2, 512), (128, 2, 1, 256)])
 @pytest.mark.parametrize("causal", [True, False])
@@ -398,11 +427,12 @@ def test_flash_attention_bwd_dq_variants(variant, cfg, D, Hq, Hkv, S, causal):
         lib().flash_attn_set_dkdv_cfg(old_cfg)
 
 
+@pytest.mark.parametrize("shape", [43, 44, 83, 143, 183])
 @pytest.mark.parametrize("B,S,Hq,Hkv", [(2, 256, 4, 4), (2, 1024, 12, 12), (1, 512, 8, 2), (2, 768, 6, 3)])
 @pytest.mark.parametrize("causal", [True, False])
-def test_flash_attention_bwd_d64_two_wave(B, S, Hq, Hkv, causal):
-    """The D = 64 dK/dV kernel with two waves per SIMD (cfg 68, csrc/flash_bwd_d64.hip) against the fp32 autograd
-    reference -- direct bf16 dK / dV (Hq == Hkv) and the fp32-partial GQA path -- and against the one-wave kernel
+def test_flash_attention_bwd_d64_two_wave(shape, B, S, Hq, Hkv, causal):
+    """The D = 64 dK/dV kernel with two waves per SIMD (cfg 68, csrc/flash_bwd_d64.hip; every workgroup shape) against
+    the fp32 autograd reference -- direct bf16 dK / dV (Hq == Hkv) and the fp32-partial GQA path -- and against the one-wave kernel
     (cfg 67): the same products in another summation order, so the gradients agree to bf16 rounding."""
     from kubeoperator_amd.ops.functional import rope_attention
     from kubeoperator_amd.ops.reference import attention_ref
@@ -413,6 +443,7 @@ def test_flash_attention_bwd_d64_two_wave(B, S, Hq, Hkv, causal):
     do = torch.randn(B * S, Hq * D, device=DEV, dtype=torch.bfloat16)
     grads = {}
     old_cfg = lib().flash_attn_set_dkdv_cfg(68)
+    old_shape = lib().flash_attn_set_d64_shape(shape)
     try:
         for cfg in (67, 68):
             lib().flash_attn_set_dkdv_cfg(cfg)
@@ -422,6 +453,7 @@ def test_flash_attention_bwd_d64_two_wave(B, S, Hq, Hkv, causal):
             grads[cfg] = qkv.grad.float()
     finally:
         lib().flash_attn_set_dkdv_cfg(old_cfg)
+        lib().flash_attn_set_d64_shape(old_shape)
     x = qkv0.float().requires_grad_(True)
     a, c = Hq * D, (Hq + Hkv) * D
     of, _ = attention_ref(x[:, :a], x[:, a:c], x[:, c:], B, S, Hq, Hkv, D, causal)

@@ -59,3 +59,63 @@ def test_lag_without_reference_hold_reproduces_divergence(monkeypatch):
     _, on = _train("tiny_llama", True, 1, monkeypatch, hold=False)
     rel = ((on - off).norm() / (off - init).norm()).item()
     assert rel > 2e-2, rel
+
+
+@pytest.mark.parametrize("frozen_bias", [True, False])
+def test_layernorm_side_fold_only_into_main_grad_views(frozen_bias, monkeypatch):
+    """The LayerNorm weight/bias fold goes to the weight-gradient stream only when BOTH outputs are main_grad views:
+    with a frozen bias its output is a temporary, which the compute stream's allocator could hand out again while the
+    lagging side-stream kernel still writes it. Either way dw / db match the one-stream result."""
+    from kubeoperator_amd.ops import functional as kf
+
+    calls = []
+
+    class _Store:
+        wgrad_stream = True
+        _side = torch.cuda.Stream()
+
+        def side_stream(self):
+            return self._side
+
+        def hold_side(self, inputs):  # the real store keeps them referenced until the side stream passes them
+            pass
+
+        def await_param(self, p):  # no optimizer stream here
+            pass
+
+    class _Hooks:
+        store = _Store()
+
+        def accumulate_for(self, p):
+            return False
+
+        def ready(self, p):
+            pass
+
+    real_launch = kf._side_launch
+    monkeypatch.setattr(kf, "_side_launch", lambda w, launch, *inp: (calls.append(1), real_launch(w, launch, *inp)))
+    monkeypatch.setattr(kf, "SIDE_LAG_CYCLES", 1_000_000)
+    torch.manual_seed(3)
+    H, T = 768, 512
+    x = torch.randn(T, H, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    w = torch.nn.Parameter(1 + 0.1 * torch.randn(H, device="cuda").to(torch.bfloat16))
+    b = torch.nn.Parameter(0.1 * torch.randn(H, device="cuda").to(torch.bfloat16), requires_grad=not frozen_bias)
+    w.main_grad = torch.zeros_like(w)
+    w._kop_hooks = _Hooks()
+    if not frozen_bias:
+        b.main_grad = torch.zeros_like(b)
+        b._kop_hooks = w._kop_hooks
+    dy = torch.randn(T, H, device="cuda", dtype=torch.bfloat16)
+    y = kf.layer_norm(x, w, b)
+    y.backward(dy)
+    junk = [torch.full((H,), 7.0, device="cuda", dtype=torch.bfloat16) for _ in range(64)]  # reuse freed blocks
+    torch.cuda.synchronize()
+    assert (len(calls) == 0) == frozen_bias
+    xf = x.detach().float().requires_grad_(True)
+    wf = w.detach().float().requires_grad_(True)
+    bf = b.detach().float().requires_grad_(True)
+    torch.nn.functional.layer_norm(xf, (H,), wf, bf, 1e-5).backward(dy.float())
+    assert (w.main_grad.float() - wf.grad).norm() / wf.grad.norm() < 2e-2
+    if not frozen_bias:
+        assert (b.main_grad.float() - bf.grad).norm() / bf.grad.norm() < 2e-2
+    del junk

@@ -1,6 +1,6 @@
 """Bandwidth of the HIP bf16 transpose at the shapes of a Llama-3-8B step (weight-gradient operands and
-W^T refresh). KOP_TRANSPOSE=square selects the 64x64-tile kernel, =cols the 64x128 kernel in column-tile order; the
-default is the 64x128 kernel in row-tile order.
+W^T refresh): the 64x128-tile kernel in row-tile order (the 64x64-tile and column-order forms it was measured against
+in round 4 are no longer built).
 
 usage: python tools/bench_transpose.py
 """
@@ -17,7 +17,7 @@ SHAPES = [(8192, 4096), (8192, 6144), (8192, 14336), (8192, 28672), (4096, 14336
 
 
 def main():
-    res = {"mode": os.environ.get("KOP_TRANSPOSE", "rows")}
+    res = {"mode": "rows"}
     for R, C in SHAPES:
         x = torch.randn(R, C, device="cuda").to(torch.bfloat16)
         y = torch.empty(C, R, device="cuda", dtype=torch.bfloat16)

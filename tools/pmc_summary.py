@@ -18,7 +18,9 @@ Derived per dispatch:
 * ``clk_GHz`` = kernel cycles / wall time (the clock the chip held; profiled passes clock 2-5 % lower than unprofiled);
 * ``mfma_TFs`` = MFMA FLOPs / wall time, with FLOPs = busy cycles x 1,024 (a dense bf16 MFMA does 1,024 FLOP per SIMD
   cycle: 32,768 per 32-cycle 32x32x16) -- comparable with the 2,500 TF/s dense bf16 peak at 2.4 GHz;
-* wave-cycle fractions (``WAIT_ANY/wc`` ...) as before (SQ wave counters count in the same units, ratios are safe).
+* wave-cycle fractions (``WAIT_ANY/wc`` ...) as before (SQ wave counters count in the same units, ratios are safe);
+* ``FETCH_SIZE`` / ``WRITE_SIZE`` (KB per dispatch) as MB and TB/s over the dispatch's wall time, and
+  ``l2_hit`` = TCC_HIT / (TCC_HIT + TCC_MISS) when both passes ran.
 """
 import collections
 import csv
@@ -66,6 +68,16 @@ def main(paths):
                 v, w = per(k, n), per(k, "SQ_WAVE_CYCLES")
                 if v is not None and w:
                     line.append(f"{n[3:]}/wc={v / w:.3f}")
+        # HBM-side traffic (rocprofv3 derived counters, KB per dispatch) and the L2 hit rate
+        for n, tag in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+            v = per(k, n)
+            if v is not None:
+                line.append(f"{tag}_MB={v / 1024:.1f}")
+                if dur:
+                    line.append(f"{tag}_TBs={v * 1024 / dur * 1e-12:.2f}")
+        hit, miss = per(k, "TCC_HIT_sum"), per(k, "TCC_MISS_sum")
+        if hit is not None and miss is not None and hit + miss > 0:
+            line.append(f"l2_hit={hit / (hit + miss):.3f}")
         for n in ("SQ_INSTS_MFMA", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_VMEM", "SQ_LDS_BANK_CONFLICT"):
             v = per(k, n)
             if v is not None:

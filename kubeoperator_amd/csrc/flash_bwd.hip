@@ -1033,16 +1033,18 @@ static void launch_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const 
     // one wave per SIMD (flash_bwd_w1.hip): query-major dS staged through LDS into whole-line stores, in the
     // wave-block layout (cfg 64; 640 = the same at D = 64, opt-in) or plain rows (66); cfg 67 / 670: key-major tiles
     // stored straight from the accumulators (no LDS staging), read back transposed by the dQ kernel
-    // (the default 67 takes the key-major path at D = 64 as well: GPT-2-small backward at its bench shape 0.372 /
-    // 0.373 ms vs 0.402 / 0.400 with the two-waves-per-SIMD kernel, step +1.1 %: profiles/r4_gpt2_kmaj_d64_ab.jsonl)
-    const bool kmaj = (D == 128 && cfg == 67) || (D == 64 && (cfg == 67 || cfg == 670));
+    // (at D = 64 the one-wave kernel is opt-in as 670 since round 6: the default 67 runs flash_bwd_d64.hip there;
+    // the one-wave kernel had beaten the older 4-wave cfg 42 kernel 0.372 vs 0.402 ms: profiles/r4_gpt2_kmaj_d64_ab.jsonl)
+    const bool kmaj = (D == 128 && cfg == 67) || (D == 64 && cfg == 670);
     const bool one_wave = S % 256 == 0 && ((D == 128 && (cfg == 64 || cfg == 66 || cfg == 67)) ||
-                                           (D == 64 && (cfg == 640 || cfg == 670 || cfg == 67)));
+                                           (D == 64 && (cfg == 640 || cfg == 670)));
     const bool blk = one_wave && cfg != 66;
     bool done = false;
     int np = direct ? 0 : Hq / Hkv;  // fp32 partials per GQA group left for the finalize pass
-    // cfg 68: the D = 64 dK/dV kernel with two waves per SIMD (flash_bwd_d64.hip), key-major dS tiles
-    const bool w2 = D == 64 && cfg == 68 && S % 256 == 0;
+    // cfg 68 (and the default 67 at D = 64): the D = 64 dK/dV kernel with two waves per SIMD (flash_bwd_d64.hip),
+    // key-major dS tiles. GPT-2-small shape causal backward 0.335-0.345 ms vs 0.373-0.387 with the one-wave kernel
+    // (cfg 670), step +0.5-0.9 % (profiles/r6_gpt2_dkdv68_step_ab.jsonl)
+    const bool w2 = D == 64 && (cfg == 68 || cfg == 67) && S % 256 == 0;
     if (w2) {
       np = flash_attn_bwd_dkdv_d64(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs,
                                    dos, dks, dvs, scale, cflag, stream);

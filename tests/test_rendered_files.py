@@ -17,11 +17,20 @@ import pytest
 import tomli
 import yaml
 
-from kubeoperator_amd.control.domain import deploy
+from kubeoperator_amd.control.domain import clusters, deploy, hosts
 from kubeoperator_amd.control.engine import filecheck
-from test_control_lifecycle import _cluster
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _cluster():
+    """1 master (m1) + 1 GPU worker (w1) on the SimFarm of the ``control`` fixture."""
+    for hn, ip in (("m1", "10.0.0.1"), ("w1", "10.0.0.2")):
+        hosts.create_host({"name": hn, "ip": ip, "password": "pw"})
+    clusters.create_cluster({"name": "demo", "template": "single-master", "network_plugin": "flannel",
+                             "persistent_storage": "local-volume"})
+    clusters.add_node("demo", {"name": "m1", "host": "m1", "roles": ["master"]})
+    clusters.add_node("demo", {"name": "w1", "host": "w1", "roles": ["worker"]})
 
 
 def _install(control):

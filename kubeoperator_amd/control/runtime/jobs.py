@@ -27,7 +27,7 @@ import time
 import traceback
 import uuid
 
-from sqlalchemy import select, update
+from sqlalchemy import delete, select, update
 
 from ..store import models as M
 from ..store.db import session_scope
@@ -245,14 +245,15 @@ def claim_pending(jid: str) -> M.Job:
 
 
 def run_claimed(job: M.Job, heartbeat_s: float = INLINE_HEARTBEAT_S) -> dict:
-    """``run_job`` for an inline-owned job (``add_job(inline=True)`` / ``claim_pending``): a daemon thread beats the inline worker's row
-    every ``heartbeat_s`` until the job ends, then the row is marked stopped."""
+    """``run_job`` for an inline-owned job (``add_job(inline=True)`` / ``claim_pending``): a daemon thread beats the inline
+    worker's row every ``heartbeat_s`` until the job ends; the row is then deleted (it existed only to prove the run
+    alive, and the task monitor lists worker processes, not finished inline runs)."""
     stop = threading.Event()
 
-    def beat(**extra):
+    def beat():
         with session_scope() as s:
             s.execute(update(M.WorkerHeartbeat).where(M.WorkerHeartbeat.name == job.worker)
-                      .values(last_seen=M.now(), **extra))
+                      .values(last_seen=M.now()))
 
     def loop():
         while not stop.wait(heartbeat_s):
@@ -269,9 +270,10 @@ def run_claimed(job: M.Job, heartbeat_s: float = INLINE_HEARTBEAT_S) -> dict:
         stop.set()
         t.join(heartbeat_s + 1.0)
         try:
-            beat(active=[], processed=1, stopped=True)
+            with session_scope() as s:
+                s.execute(delete(M.WorkerHeartbeat).where(M.WorkerHeartbeat.name == job.worker))
         except Exception:  # noqa: BLE001
-            log.exception("inline heartbeat failed")
+            log.exception("retiring the inline worker row failed")
 
 
 def _pid_alive(pid: int) -> bool:

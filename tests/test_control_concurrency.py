@@ -180,6 +180,8 @@ def test_inline_run_is_not_an_orphan(control):
     _release.set()
     t.join(30)
     assert out["state"] == "SUCCESS"
+    with session_scope() as s:  # the inline runner's liveness row is retired with its run
+        assert s.get(M.WorkerHeartbeat, j.worker) is None
 
 
 def test_dead_worker_jobs_and_executions_are_recovered(control):

@@ -170,7 +170,8 @@ def main() -> int:
     timing = cuda and collectives_on(info)
     if timing:  # exposed-communication events (a handful per step, no host synchronisation)
         trainer.dp.finish_waits, trainer.store.gate_waits = [], []
-        trainer.dp.timeline = []
+        # per-bucket timeline (ready events + RCCL's own durations); KOP_BENCH_TIMELINE=0 turns it off (A/B)
+        trainer.dp.timeline = [] if os.environ.get("KOP_BENCH_TIMELINE", "1") != "0" else None
     comm0, gather0 = trainer.dp.comm_bytes, trainer.dp.gather_bytes
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -194,7 +195,7 @@ def main() -> int:
 
         rec = {"rank": info.rank, "affinity": affinity, "finish_wait_ms": round(fin, 3), "gate_wait_ms": round(gate, 3),
                "gate_waits_per_step": len(trainer.store.gate_waits) // max(1, args.steps),
-               "buckets": timeline_summary(trainer.dp.timeline)}
+               "buckets": timeline_summary(trainer.dp.timeline) if trainer.dp.timeline is not None else None}
         ranks = gather_objects(rec, info)
         trainer.dp.finish_waits = trainer.store.gate_waits = trainer.dp.timeline = None
     streams = stream_inventory(trainer, collectives_on(info)) if cuda else None

@@ -104,11 +104,37 @@ def write_scope():
             s.close()
 
 
+def _retire_duplicate_active_executions() -> int:
+    """Before the one-active-execution index is added to an older store: a cluster holding several PENDING / STARTED
+    deploy executions (possible before the lock was atomic) keeps its newest, the others are marked FAILURE."""
+    n = 0
+    with session_scope() as s:
+        rows = list(s.scalars(select(M.Execution).where(M.Execution.kind == "deploy",
+                                                        M.Execution.state.in_(("PENDING", "STARTED")))
+                              .order_by(M.Execution.project_id, M.Execution.date_created.desc())))
+        seen = set()
+        for e in rows:
+            if e.project_id in seen:
+                e.state, e.date_end = "FAILURE", M.now()
+                e.result_summary = {"error": "superseded: a newer operation was active when the store was upgraded"}
+                n += 1
+            seen.add(e.project_id)
+    return n
+
+
 def ensure_indexes() -> None:
     """Create indexes added after a store's tables were first created (``create_all`` skips existing tables)."""
+    from sqlalchemy import inspect as sa_inspect
+
     eng = engine()
+    insp = sa_inspect(eng)
     for t in M.Base.metadata.sorted_tables:
+        existing = {ix["name"] for ix in insp.get_indexes(t.name)} if insp.has_table(t.name) else set()
         for ix in t.indexes:
+            if ix.name in existing:
+                continue
+            if ix.name == "uq_one_active_deploy_per_project":
+                _retire_duplicate_active_executions()
             ix.create(eng, checkfirst=True)
 
 

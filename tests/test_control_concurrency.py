@@ -213,3 +213,41 @@ def test_dead_worker_jobs_and_executions_are_recovered(control):
         assert deploy.get(eid)["state"] == "FAILURE"
     assert jobs.get("live-job").state == "STARTED"
     deploy.create("demo", "gpu-validate", run="none")  # the cluster is free again
+
+
+def test_index_added_to_an_older_store_retires_duplicate_active_executions(tmp_path, monkeypatch):
+    """A store created before the one-active-execution index (several PENDING deploy executions of one cluster, as the
+    old unlocked check allowed) still starts: the newest stays active, the others are marked FAILURE, the index is
+    created and enforced from then on."""
+    import sqlite3
+
+    from sqlalchemy.exc import IntegrityError
+
+    from kubeoperator_amd.control.conf import Config, set_config
+    from kubeoperator_amd.control.store import db
+
+    monkeypatch.setenv("KOP_PBKDF2_ITERS", "1000")
+    cfg = Config(path=None)
+    cfg["DATA_DIR"] = str(tmp_path / "data")
+    set_config(cfg)
+    db.configure(cfg.db_url)
+    db.init_db()
+    c = clusters.create_cluster({"name": "old", "template": "single-master"})
+    pid = clusters.get_cluster(c["name"]).project_id
+    path = cfg.db_url.split("///", 1)[1]
+    con = sqlite3.connect(path)
+    con.execute("DROP INDEX uq_one_active_deploy_per_project")
+    for i, t in enumerate(("2020-01-01 00:00:00", "2020-01-02 00:00:00", "2020-01-03 00:00:00")):
+        con.execute("INSERT INTO executions (id, kind, project_id, operation, params, steps, current_step, state, num, "
+                    "timedelta, result_summary, result_raw, created_by, date_created) VALUES "
+                    "(?, 'deploy', ?, 'install', '{}', '[]', 0, 'PENDING', 1, 0, '{}', '{}', '', ?)", (f"e{i}", pid, t))
+    con.commit()
+    con.close()
+    db.configure(cfg.db_url)
+    db.init_db()
+    with session_scope() as s:
+        states = {e.id: e.state for e in s.scalars(select(M.Execution).where(M.Execution.project_id == pid))}
+    assert states == {"e0": "FAILURE", "e1": "FAILURE", "e2": "PENDING"}
+    with pytest.raises(IntegrityError):
+        with session_scope() as s:
+            s.add(M.Execution(kind="deploy", project_id=pid, operation="upgrade", state="STARTED"))

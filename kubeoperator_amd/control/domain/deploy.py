@@ -36,7 +36,7 @@ from ..engine.trace import summary as trace_summary
 from ..runtime import jobs, metrics
 from ..store import models as M
 from ..store.db import session_scope, write_scope
-from . import clusters, context, plan
+from . import clusters, plan
 
 log = logging.getLogger("kubeoperator.deploy")
 

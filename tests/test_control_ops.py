@@ -10,7 +10,7 @@ import threading
 
 import pytest
 
-from kubeoperator_amd.control.domain import backup, cloud, clusters, deploy, messages, monitor
+from kubeoperator_amd.control.domain import backup, cloud, clusters, deploy, monitor
 from kubeoperator_amd.control.store import models as M
 from kubeoperator_amd.control.store.db import session_scope
 

@@ -599,6 +599,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("flash_attn_set_fwd_variant", [](int64_t v) { return (int64_t)kop::flash_attn_set_fwd_variant((int)v); });
   m.def("decode_attn_set_mfma", [](int64_t on) { return (int64_t)kop::decode_attn_set_mfma((int)on); });
   m.def("flash_attn_set_dkdv_cfg", [](int64_t c) { return (int64_t)kop::flash_attn_set_dkdv_cfg((int)c); });
+  m.def("flash_attn_set_dq_nw", [](int64_t c) { return (int64_t)kop::flash_attn_set_dq_nw((int)c); });
   m.def("flash_attn_set_d64_shape", [](int64_t c) { return (int64_t)kop::flash_attn_set_d64_shape((int)c); });
   m.def("flash_attn_set_dkdv_hpw", [](int64_t h) { return (int64_t)kop::flash_attn_set_dkdv_hpw((int)h); });
 }

@@ -709,13 +709,17 @@ __global__ void __launch_bounds__(512, 1) fa_bwd_dq8_kernel(
 // are one such tile, copied lane-linear into LDS and read with ds_read_b64_tr_b16 -- lane 4q + p of a 16-lane group
 // names key row q (4 consecutive elements = 4 queries); the XOR spreads one 32-lane half's 32 reads over all 64 banks.
 // The two transposed reads of a k-step take keys R0 + 4hh + 0..3 and R0 + 8 + 4hh + 0..3, the K^T operand's k order.
-template <int D, int HP, bool BLK = false, bool NTL = false, bool KMAJ = false>
-__global__ void __launch_bounds__(512, 1) fa_bwd_dq_ds_kernel(const bf16_t* __restrict__ ds, const bf16_t* __restrict__ k,
-                                                              bf16_t* __restrict__ dq, int B, int S, int Hq, int Hkv,
-                                                              int64_t ks, int64_t dqs, float scale, int causal) {
-  // HP q-heads of one GQA group per workgroup (RH = 256/HP query rows each) share every K tile: the
+// NW: waves per workgroup (32 query rows each). 8: one 512-thread workgroup per CU; 4: two 256-thread workgroups per
+// CU (at D = 64 a 3-slot ring is 72 KB), so one workgroup's ramp-up / drain overlaps the other's stream.
+template <int D, int HP, bool BLK = false, bool NTL = false, bool KMAJ = false, int NW = 8>
+__global__ void __launch_bounds__(NW * 64, 1) fa_bwd_dq_ds_kernel(const bf16_t* __restrict__ ds,
+                                                                  const bf16_t* __restrict__ k, bf16_t* __restrict__ dq,
+                                                                  int B, int S, int Hq, int Hkv, int64_t ks, int64_t dqs,
+                                                                  float scale, int causal) {
+  // HP q-heads of one GQA group per workgroup (RH = 32 NW / HP query rows each) share every K tile: the
   // kernel streams dS, so K re-reads from L2/MALL are the traffic worth cutting
-  constexpr int NW = 8, BM = 256, RH = BM / HP, WPH = NW / HP, BN = 64, ROWB = D * 2, NSLOT = 3;
+  constexpr int BM = 32 * NW, RH = BM / HP, WPH = NW / HP, BN = 64, ROWB = D * 2, NSLOT = 3;
+  static_assert(NW % HP == 0, "every wave within one head");
   constexpr int KT = BN * ROWB, DST = BM * BN * 2, SLOT = KT + DST;
   constexpr int PPW = (KT / 1024) / NW + (DST / 1024) / NW;  // DMA pieces per wave per tile
   static_assert((KT / 1024) % NW == 0 && (DST / 1024) % NW == 0, "tiles must split evenly over the waves");
@@ -855,23 +859,45 @@ static bool dq_nt() {
   return on;
 }
 
-template <int D, int HP, bool BLK, bool NTL, bool KMAJ = false>
+template <int D, int HP, bool BLK, bool NTL, bool KMAJ = false, int NW = 8>
 static void launch_dq_ds_nt(const bf16_t* ds, const bf16_t* k, bf16_t* dq, int B, int S, int Hq, int Hkv, int64_t ks,
                             int64_t dqs, float scale, bool causal, hipStream_t stream) {
-  const size_t lds = 3 * (64 * (D * 2) + 256 * 64 * 2);
+  const size_t lds = 3 * (64 * (D * 2) + 32 * NW * 64 * 2);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)fa_bwd_dq_ds_kernel<D, HP, BLK, NTL, KMAJ>,
+    (void)hipFuncSetAttribute((const void*)fa_bwd_dq_ds_kernel<D, HP, BLK, NTL, KMAJ, NW>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
-  fa_bwd_dq_ds_kernel<D, HP, BLK, NTL, KMAJ><<<B * (Hq / HP) * (S / (256 / HP)), 512, lds, stream>>>(
+  fa_bwd_dq_ds_kernel<D, HP, BLK, NTL, KMAJ, NW><<<B * (Hq / HP) * (S / (32 * NW / HP)), NW * 64, lds, stream>>>(
       ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal);
+}
+
+// waves per dQ workgroup: KOP_DQ_NW (4 / 8; 0 = automatic: 4 at D = 64 with at most 4 heads per workgroup, else 8)
+static int g_dq_nw = -1;
+int flash_attn_set_dq_nw(int v) {
+  if (g_dq_nw < 0) {
+    const char* e = getenv("KOP_DQ_NW");
+    g_dq_nw = e ? atoi(e) : 0;
+  }
+  const int old = g_dq_nw;
+  if (v >= 0) g_dq_nw = v;
+  return old;
 }
 
 template <int D, int HP, bool BLK = false, bool KMAJ = false>
 static void launch_dq_ds(const bf16_t* ds, const bf16_t* k, bf16_t* dq, int B, int S, int Hq, int Hkv, int64_t ks,
                          int64_t dqs, float scale, bool causal, hipStream_t stream) {
+  const int req = flash_attn_set_dq_nw(-1);
+  const bool nw4 = HP <= 4 && S % 128 == 0 && (req == 4 || (req == 0 && D == 64));
+  if constexpr (HP <= 4) {
+    if (nw4) {
+      if (dq_nt()) launch_dq_ds_nt<D, HP, BLK, true, KMAJ, 4>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+      else launch_dq_ds_nt<D, HP, BLK, false, KMAJ, 4>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
+      return;
+    }
+  }
+  (void)nw4;
   if (dq_nt()) launch_dq_ds_nt<D, HP, BLK, true, KMAJ>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
   else launch_dq_ds_nt<D, HP, BLK, false, KMAJ>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);
 }

@@ -29,7 +29,7 @@ namespace kop {
 // NW waves per workgroup (BN = 32 NW keys), NS-slot stage ring (prefetch distance NS - 1).
 // DIAG (timing ablations, WRONG results; instantiated only in the -DKOP_ABLATIONS probe build): 1 no dS stores,
 // 2 no exponentials, 4 no stage barrier, 16 no dV / dK products, 32 no S / dP products.
-template <bool DIRECT, int NW, int NS, int DIAG = 0, bool PAIR = false>
+template <bool DIRECT, int NW, int NS, int DIAG = 0>
 __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_d64_kernel(
     const bf16_t* __restrict__ q, const bf16_t* __restrict__ k, const bf16_t* __restrict__ v,
     const bf16_t* __restrict__ dout, const float* __restrict__ nlse, const float* __restrict__ ndelta,
@@ -46,37 +46,12 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_d64_kernel(
   const int r = lane & 31, hh = lane >> 5;
   const int tq = (lane & 15) >> 2, tp = lane & 3, tg1 = (lane >> 4) & 1;
   const int grp = Hq / Hkv, nkb = S / BN;
-  // work: PAIR -- key blocks p and nkb-1-p of one (batch, head) in sequence (equal work per workgroup under a causal
-  // mask), the workgroups of a head adjacent in one XCD's dispatch order so they sweep its Q / dO stages together
-  // (L2 hits instead of HBM / MALL re-reads); else one key block, heaviest first (attn_work)
-  int b, hq, kb_first, nunits;
-  if constexpr (PAIR) {
-    const int npair = nkb / 2, G = B * Hq;
-    const int bid = blockIdx.x;
-    int g, pr;
-    if ((G & 7) == 0) {
-      const int xcd = bid & 7, sx = bid >> 3;
-      g = (sx / npair) * 8 + xcd;
-      pr = sx % npair;
-    } else {
-      g = bid / npair;
-      pr = bid % npair;
-    }
-    b = g / Hq;
-    hq = g % Hq;
-    kb_first = pr;
-    nunits = 2;
-  } else {
-    const AttnWork aw = attn_work(blockIdx.x, B, Hq, grp, nkb);
-    b = aw.b;
-    hq = aw.unit;
-    kb_first = aw.rank;  // heaviest key blocks (earliest keys under a causal mask) first
-    nunits = 1;
-  }
+  const AttnWork aw = attn_work(blockIdx.x, B, Hq, grp, nkb);
+  const int kb = aw.rank;  // heaviest key blocks (earliest keys under a causal mask) first
+  const int b = aw.b, hq = aw.unit;
   const int kvh = hq / grp;
   const float c2 = scale * 1.4426950408889634f;
-  for (int un = 0; un < nunits; ++un) {
-    const int kb = un == 0 ? kb_first : nkb - 1 - kb_first;
+  {
     const int k0 = kb * BN, k0w = k0 + 32 * wid;
     const int nqt = S / BQ;
     const int qt0 = causal ? k0 / BQ : 0;        // the workgroup's lowest stage
@@ -333,31 +308,31 @@ __global__ void __launch_bounds__(NW * 64, 2) fa_bwd_dkdv_d64_kernel(
       }
     };
     out(k0w + r);
-    __builtin_amdgcn_s_barrier();  // every wave is done with the ring before the next key block's DMA refills it
   }
 }
 
-template <int NW, int NS, int DIAG = 0, bool PAIR = false>
+template <int NW, int NS, int DIAG = 0>
 static int launch_d64(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* dout, const float* nlse,
                       const float* ndelta, float* dk_part, float* dv_part, bf16_t* dk, bf16_t* dv, bf16_t* ds, int B, int S,
                       int Hq, int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t dos, int64_t dks, int64_t dvs,
                       float scale, int causal, hipStream_t stream) {
   constexpr size_t lds = NS * (2 * 32 * 128 + 1024);
-  const dim3 grid(B * Hq * (S / (32 * NW)) / (PAIR ? 2 : 1));
+  const dim3 grid(B * Hq * (S / (32 * NW)));
   if (Hq == Hkv) {
-    fa_bwd_dkdv_d64_kernel<true, NW, NS, DIAG, PAIR><<<grid, NW * 64, lds, stream>>>(
+    fa_bwd_dkdv_d64_kernel<true, NW, NS, DIAG><<<grid, NW * 64, lds, stream>>>(
         q, k, v, dout, nlse, ndelta, reinterpret_cast<float*>(dk), reinterpret_cast<float*>(dv), ds, B, S, Hq, Hkv, qs,
         ks, vs, dos, scale, causal, dks, dvs);
     return 0;
   }
-  fa_bwd_dkdv_d64_kernel<false, NW, NS, DIAG, PAIR><<<grid, NW * 64, lds, stream>>>(
+  fa_bwd_dkdv_d64_kernel<false, NW, NS, DIAG><<<grid, NW * 64, lds, stream>>>(
       q, k, v, dout, nlse, ndelta, dk_part, dv_part, ds, B, S, Hq, Hkv, qs, ks, vs, dos, scale, causal, 0, 0);
   return Hq / Hkv;
 }
 
 // workgroup shape (KOP_D64_SHAPE, A/B): 43 (default) 4 waves x 32 keys (two workgroups per CU, each with its own
 // barriers), 3-slot ring; 44 the same with 4 slots; 83 8 waves (one workgroup per CU), 3 slots. GPT-2 shape causal
-// backward 0.335 / 0.338 ms (43) vs 0.343 / 0.345 (44) and 0.343 / 0.347 (83), same box alternating.
+// backward 0.335 / 0.338 ms (43) vs 0.343 / 0.345 (44) and 0.343 / 0.347 (83), same box alternating. (Key-block
+// pairs per workgroup with a head's workgroups adjacent in one XCD measured 0.347: removed, profiles/r6_experiments.md.)
 static int g_d64_shape = -1;  // -1: read KOP_D64_SHAPE on first use
 int flash_attn_set_d64_shape(int v) {
   if (g_d64_shape < 0) {
@@ -394,12 +369,6 @@ int flash_attn_bwd_dkdv_d64(const bf16_t* q, const bf16_t* k, const bf16_t* v, c
   if (shape == 83)
     return launch_d64<8, 3>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs, dos,
                             dks, dvs, scale, causal, stream);
-  if (shape == 143)  // key-block pairs, head-major in each XCD
-    return launch_d64<4, 3, 0, true>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs,
-                                     dos, dks, dvs, scale, causal, stream);
-  if (shape == 183 && (S / 256) % 2 == 0)
-    return launch_d64<8, 3, 0, true>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs,
-                                     dos, dks, dvs, scale, causal, stream);
   if (shape == 44)
     return launch_d64<4, 4>(q, k, v, dout, nlse, ndelta, dk_part, dv_part, dk, dv, ds, B, S, Hq, Hkv, qs, ks, vs, dos,
                             dks, dvs, scale, causal, stream);

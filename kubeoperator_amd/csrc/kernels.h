@@ -105,7 +105,9 @@ int flash_attn_bwd_dkdv_d64(const bf16_t* q, const bf16_t* k, const bf16_t* v, c
                             const float* ndelta, float* dk_part, float* dv_part, bf16_t* dk, bf16_t* dv, bf16_t* ds,
                             int B, int S, int Hq, int Hkv, int64_t qs, int64_t ks, int64_t vs, int64_t dos, int64_t dks,
                             int64_t dvs, float scale, int causal, hipStream_t stream);
-// workgroup shape of the D = 64 kernel (43 default, 44, 83, 143 / 183 key-block pairs); v < 0 only reads it
+// waves per dQ-from-dS workgroup: 4 / 8, 0 automatic (4 at D = 64); v < 0 only reads it
+int flash_attn_set_dq_nw(int v);
+// workgroup shape of the D = 64 kernel (43 default, 44, 83); v < 0 only reads it
 int flash_attn_set_d64_shape(int v);
 int flash_attn_bwd(const bf16_t* q, const bf16_t* k, const bf16_t* v, const bf16_t* o, const bf16_t* dout,
                    const float* lse, bf16_t* dq, bf16_t* dk, bf16_t* dv, void* workspace, int B, int S, int Hq,

@@ -873,7 +873,10 @@ static void launch_dq_ds_nt(const bf16_t* ds, const bf16_t* k, bf16_t* dq, int B
       ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal);
 }
 
-// waves per dQ workgroup: KOP_DQ_NW (4 / 8; 0 = automatic: 4 at D = 64 with at most 4 heads per workgroup, else 8)
+// waves per dQ workgroup: KOP_DQ_NW (4 / 8; 0 = automatic: 4 for a causal D = 64 backward with at most 4 heads per
+// workgroup, else 8). GPT-2 shape causal backward 0.338 / 0.339 ms with 4 vs 0.342 / 0.342 with 8, non-causal 2-3 %
+// slower with 4; at D = 128 a 4-wave workgroup's ring leaves no room for a second one per CU: the Llama-3-8B shape
+// runs 1.80 vs 1.65 ms (profiles/r6_dq_nw_bchunk_gpt2_ab.jsonl, profiles/r6_dq_nw_llama_ab.jsonl)
 static int g_dq_nw = -1;
 int flash_attn_set_dq_nw(int v) {
   if (g_dq_nw < 0) {
@@ -889,7 +892,7 @@ template <int D, int HP, bool BLK = false, bool KMAJ = false>
 static void launch_dq_ds(const bf16_t* ds, const bf16_t* k, bf16_t* dq, int B, int S, int Hq, int Hkv, int64_t ks,
                          int64_t dqs, float scale, bool causal, hipStream_t stream) {
   const int req = flash_attn_set_dq_nw(-1);
-  const bool nw4 = HP <= 4 && S % 128 == 0 && (req == 4 || (req == 0 && D == 64));
+  const bool nw4 = HP <= 4 && S % 128 == 0 && (req == 4 || (req == 0 && D == 64 && causal));
   if constexpr (HP <= 4) {
     if (nw4) {
       if (dq_nt()) launch_dq_ds_nt<D, HP, BLK, true, KMAJ, 4>(ds, k, dq, B, S, Hq, Hkv, ks, dqs, scale, causal, stream);

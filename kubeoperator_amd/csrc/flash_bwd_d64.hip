@@ -8,7 +8,8 @@
 // of resident K / V fragments, so two waves fit on every SIMD (256 registers each) and the softmax VALU of one
 // wave issues beside the other wave's MFMAs.
 //
-// One 512-thread workgroup = 8 waves = 256 keys of one (batch, q-head); wave w owns keys k0 + 32w .. +31.
+// A workgroup of NW waves owns 32 NW keys of one (batch, q-head); wave w owns keys k0 + 32w .. +31. The default
+// shape is 4 waves (two workgroups per CU, each with its own barriers); 8 waves (one per CU) measured 2 % slower.
 // Per 32-query stage and wave (all products on v_mfma_f32_32x32x16_bf16, key on the lane):
 //   S  = Q.K^T  - lse/scale   (4 MFMAs; A = Q rows from LDS, B = K^T fragments resident in VGPRs)
 //   dP = dO.V^T - delta       (4 MFMAs; A = dO rows from LDS, B = V^T fragments resident)
@@ -19,6 +20,8 @@
 // from the last query stage down, so every workgroup of a head reads the same stage at about the same time
 // (its lines are then still in the XCD's L2). Under a causal mask a wave computes the stages above its diagonal
 // unmasked, its one diagonal stage masked, and only joins the barriers / DMA of the stages below.
+// What bounds it (timing ablations, profiles/r6_experiments.md): the dS write stream and the stage ring -- removing
+// every MFMA saves 24 us of ~190 at the GPT-2 bench shape, removing the dS stores 50 us.
 #include <cstdlib>
 
 #include "attn_common.h"

@@ -67,19 +67,20 @@ def _side_active(w) -> bool:
             and not torch.cuda.is_current_stream_capturing())
 
 
-def _side_launch(w, launch, *inputs) -> None:
-    """Run ``launch()`` on ``w``'s weight-gradient stream once it has caught up with the compute stream; ``inputs``
-    stay alive (and their memory unreused) until that stream has passed them."""
-    store = w._kop_hooks.store
-    side = store.side_stream()
-    side.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(side):
+def _lagged(launch):
+    """``launch`` behind the forced side-stream lag (race tests; no-op by default)."""
+    def run():
         if SIDE_LAG_CYCLES > 0:
             torch.cuda._sleep(SIDE_LAG_CYCLES)
         launch()
-    for t in inputs:
-        t.record_stream(side)
-    store.hold_side(inputs)
+    return run
+
+
+def _side_launch(w, launch, *inputs, ready=()) -> None:
+    """Run ``launch()`` on ``w``'s weight-gradient stream once it has caught up with the compute stream; ``inputs``
+    stay alive (and their memory unreused) until that stream has passed them; the parameters in ``ready`` are marked
+    ready once it is issued (``FlatParamStore.side_submit``: possibly grouped with the next launches)."""
+    w._kop_hooks.store.side_submit(_lagged(launch), inputs, ready)
 
 
 def _sink(w: torch.Tensor, produce, *inputs, defer: bool = False):
@@ -117,18 +118,9 @@ def _sink(w: torch.Tensor, produce, *inputs, defer: bool = False):
         hooks.ready(w)
         return None
     if hooks.store.wgrad_stream and mg.is_cuda and not torch.cuda.is_current_stream_capturing():
-        store = hooks.store
-        side = store.side_stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            if SIDE_LAG_CYCLES > 0:
-                torch.cuda._sleep(SIDE_LAG_CYCLES)
-            produce(mg, acc)
-        for t in inputs:
-            t.record_stream(side)
-        store.hold_side(inputs)
-    else:
-        produce(mg, acc)
+        store.side_submit(_lagged(lambda: produce(mg, acc)), inputs, (w,))
+        return None
+    produce(mg, acc)
     hooks.ready(w)
     return None
 
@@ -491,6 +483,7 @@ class _Norm(Function):
         if ctx.layernorm:
             db_buf = mg_b if (mg_b is not None and not staged) else torch.empty_like(b)
         acc = w._kop_hooks.accumulate_for(w) if mg_w is not None else False
+        side_fold = False  # the side-stream fold marks w (and b) ready itself
         if ctx.box is not None and not ctx.layernorm and _t_ok(s):
             # also write dx^T: the dY operand of the weight gradient of the projection that produced x
             dx, dxt = lib.rms_norm_bwd_t(dy, s, w, rstd, dres, dw_buf, acc and not staged)
@@ -502,7 +495,9 @@ class _Norm(Function):
             # outputs are the parameters' main_grad views: a temporary bias buffer (frozen bias, no main_grad) would be
             # freed to the compute stream's allocator while the side-stream kernel still writes it
             dx, part = lib.norm_bwd_parts(dy, s, w, rstd, mean, dres, ctx.layernorm)
-            _side_launch(w, lambda: lib.norm_bwd_reduce_(part, dw_buf, db_buf, ctx.layernorm, acc), part)
+            side_fold = True
+            _side_launch(w, lambda: lib.norm_bwd_reduce_(part, dw_buf, db_buf, ctx.layernorm, acc), part,
+                         ready=(w, b) if ctx.layernorm else (w,))
         else:
             dx = lib.norm_bwd(dy, s, w, rstd, mean, dres, dw_buf, db_buf, ctx.layernorm, acc and not staged)
         if staged:
@@ -512,13 +507,15 @@ class _Norm(Function):
         dw = None
         if need_w:
             if mg_w is not None:
-                w._kop_hooks.ready(w)
+                if not side_fold:
+                    w._kop_hooks.ready(w)
             else:
                 dw = dw_buf
         db = None
         if ctx.layernorm and ctx.needs_input_grad[3]:
             if mg_b is not None:
-                b._kop_hooks.ready(b)
+                if not side_fold:
+                    b._kop_hooks.ready(b)
             else:
                 db = db_buf
         dres_out = dx if ctx.has_res else None

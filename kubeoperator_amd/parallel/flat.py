@@ -163,6 +163,11 @@ class FlatParamStore:
         # allowed only while a later micro-batch of the step follows (the trainer sets defer_ok)
         self._deferred: list = []
         self.defer_ok = False
+        # side-stream launches issued as one group (``side_submit``): every group costs the compute stream one event
+        # record, a marker packet that holds its next kernel back ~12 us on MI355X, and the side stream one wait.
+        # KOP_SIDE_BATCH launches per group (1: each launch forks on its own)
+        self.side_batch = max(1, int(os.environ.get("KOP_SIDE_BATCH", "1")))
+        self._side_q: list = []
         self.gate_waits: list | None = None  # (event, event) around collective-gate waits (exposed comm timing)
         self.wgrad_stream = False  # issue weight gradients on it (set by the trainer)
         name_to_bucket = {nm: b for b in self.buckets for nm in b.names}
@@ -231,6 +236,7 @@ class FlatParamStore:
         self.hooks.writes.clear()
 
     def begin_microbatch(self, index: int) -> None:
+        self.flush_side()  # the previous backward's queued launches mark their parameters ready in ITS micro-batch
         self.hooks.microbatch = index
         self.reset_readiness()
 
@@ -240,7 +246,8 @@ class FlatParamStore:
             return
         b.pending -= 1
         if b.pending == 0 and self.on_ready is not None:
-            if self._side is not None:
+            # (no collective this micro-batch: on_ready does nothing, and the fork would only cost a marker packet)
+            if self._side is not None and self.collectives_live():
                 # the bucket's gradients come from both streams: its collective is issued from the side stream
                 # after that stream has also caught up with everything the compute stream wrote so far
                 self._side.wait_stream(torch.cuda.current_stream())
@@ -269,6 +276,37 @@ class FlatParamStore:
             held.pop(0)
         held.append((ev, tuple(tensors)))
 
+    def side_submit(self, launch, inputs, ready=()) -> None:
+        """Queue ``launch()`` for the weight-gradient stream; ``inputs`` are the tensors it reads, ``ready`` the
+        parameters whose gradients it completes (marked ready once it is issued). Issued in groups of
+        ``side_batch``, and by ``flush_side``: every caller flushes before anything that depends on the queued
+        launches having been issued (deferred launches, the end of backward, the join)."""
+        self._side_q.append((launch, tuple(inputs), tuple(ready)))
+        if len(self._side_q) >= self.side_batch:
+            self.flush_side()
+
+    def flush_side(self) -> None:
+        """Issue the queued side-stream launches behind one fork from the compute stream: the side stream waits for
+        everything queued on the compute stream so far (a superset of what each launch reads), runs them in queue
+        order, and keeps their inputs referenced until it has passed them (``hold_side``)."""
+        q, self._side_q = self._side_q, []
+        if not q:
+            return
+        side = self.side_stream()
+        side.wait_stream(torch.cuda.current_stream())
+        # no_grad: a group flushed after backward has returned (the trainer, the next micro-batch) runs outside
+        # autograd's own no-grad context, and its GEMMs write into out= buffers from saved tensors that require grad
+        with torch.cuda.stream(side), torch.no_grad():
+            for launch, _, _ in q:
+                launch()
+        ins = [t for _, inputs, _ in q for t in inputs]
+        for t in ins:
+            t.record_stream(side)
+        self.hold_side(ins)
+        for _, _, ready in q:
+            for p in ready:
+                self.hooks.ready(p)
+
     def defer(self, launch) -> None:
         """Queue a side-stream gradient launch for ``run_deferred`` (ops.functional._sink(defer=True)).
 
@@ -279,11 +317,13 @@ class FlatParamStore:
             raise RuntimeError("weight-gradient launch deferred while bucket collectives are live: a bucket would be "
                                "reduced before its deferred gradient is written (defer_ok must be off on the "
                                "micro-batch whose backward reduces)")
+        self.flush_side()  # side-stream launches keep their issue order (tied weights: overwrite before accumulate)
         self._deferred.append(launch)
 
     def run_deferred(self) -> None:
         """Issue the deferred side-stream gradient launches (the trainer calls this once the next micro-batch's forward
         is queued; ``join_side`` flushes whatever is left)."""
+        self.flush_side()
         pending, self._deferred = self._deferred, []
         for launch in pending:
             launch()

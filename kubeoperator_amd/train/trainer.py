@@ -151,6 +151,7 @@ class Trainer:
             loss = self.model(ids, tgt)
             self.store.run_deferred()
             loss.backward()
+            self.store.flush_side()  # the last queued weight-gradient launches of this backward
             losses.append(loss.detach())
         self.store.join_side()
         self.dp.finish_grads()

@@ -30,3 +30,27 @@ def test_tune_gemms_merge_replaces_retuned_rows_in_place_and_appends_new_ones():
     assert rows[3] == committed[3] + "\n"  # skipped shape (LM head) keeps its committed winner
     assert rows[4] == "GemmTunableOp_BFloat16_NN,nn_4096_8192_6144_ld_4096_6144_4096,Default,0.3\n"
     assert len(rows) == 5 and all(r.endswith("\n") for r in rows)
+
+
+def test_stream_gaps_sums_same_stream_gaps_per_kernel_pair_inside_the_step_window():
+    sg = _tool("stream_gaps")
+    ns = 1000  # timestamps in ns
+    rows = [
+        (0, 1 * ns, "kop::clip_coef_kernel", "0"),            # step 1 starts
+        (2 * ns, 50 * ns, "gemm_a", "0"),
+        (62 * ns, 70 * ns, "gelu_bwd", "0"),                  # 12 us after gemm_a on its stream
+        (51 * ns, 90 * ns, "wgrad", "1"),                     # other stream: not a gap of stream 0
+        (101 * ns, 102 * ns, "kop::clip_coef_kernel", "0"),   # step 2 starts
+        (104 * ns, 150 * ns, "gemm_a", "0"),
+        (161 * ns, 170 * ns, "gelu_bwd", "0"),                # 11 us
+        (172 * ns, 173 * ns, "tiny", "0"),                    # 2 us: below --min-us
+        (200 * ns, 201 * ns, "kop::clip_coef_kernel", "0"),   # end of the window
+    ]
+    res = sg.stream_gaps(rows, steps=2, min_us=5.0)
+    s0 = res["0"]
+    assert abs(s0["pairs"][("gemm_a", "gelu_bwd")] - 11.5) < 1e-9  # us per step
+    assert s0["counts"][("gemm_a", "gelu_bwd")] == 2
+    # plus gelu_bwd -> the second step's clip_coef (31 us, once); the window ends at the last clip_coef
+    assert set(s0["pairs"]) == {("gemm_a", "gelu_bwd"), ("gelu_bwd", "kop::clip_coef_kernel")}
+    assert abs(s0["gap_ms"] - (12 + 11 + 31) / 2 / 1e3) < 1e-12
+    assert res["1"]["gap_ms"] == 0.0

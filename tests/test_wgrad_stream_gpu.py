@@ -14,13 +14,14 @@ pytestmark = pytest.mark.gpu
 LAG = 1_000_000  # GPU clock cycles per weight gradient
 
 
-def _train(model: str, stream: bool, accum: int, monkeypatch, hold: bool = True):
+def _train(model: str, stream: bool, accum: int, monkeypatch, hold: bool = True, batch: int = 1):
     from kubeoperator_amd.ops import functional
     from kubeoperator_amd.parallel.dist import DistInfo
     from kubeoperator_amd.parallel.flat import FlatParamStore
     from kubeoperator_amd.train import TrainConfig, Trainer
 
     monkeypatch.setenv("KOP_WGRAD_STREAM", "1" if stream else "0")
+    monkeypatch.setenv("KOP_SIDE_BATCH", str(batch))
     monkeypatch.setattr(functional, "SIDE_LAG_CYCLES", LAG if stream else 0)
     if not hold:
         monkeypatch.setattr(FlatParamStore, "hold_side", lambda self, tensors: None)
@@ -45,9 +46,12 @@ def _train(model: str, stream: bool, accum: int, monkeypatch, hold: bool = True)
 
 @pytest.mark.parametrize("model", ["tiny_llama", "tiny_gpt2"])
 @pytest.mark.parametrize("accum", [1, 4])
-def test_lagging_side_stream_matches_one_stream(model, accum, monkeypatch):
+@pytest.mark.parametrize("batch", [1, 6])
+def test_lagging_side_stream_matches_one_stream(model, accum, batch, monkeypatch):
+    """``batch``: side-stream launches grouped behind one fork (FlatParamStore.side_submit), the readiness marks and
+    the inputs' reference holds following the group."""
     init, off = _train(model, False, accum, monkeypatch)
-    _, on = _train(model, True, accum, monkeypatch)
+    _, on = _train(model, True, accum, monkeypatch, batch=batch)
     rel = ((on - off).norm() / (off - init).norm()).item()
     assert rel < 5e-3, rel
 
@@ -70,9 +74,13 @@ def test_layernorm_side_fold_only_into_main_grad_views(frozen_bias, monkeypatch)
 
     calls = []
 
+    from kubeoperator_amd.parallel.flat import FlatParamStore
+
     class _Store:
         wgrad_stream = True
         _side = torch.cuda.Stream()
+        side_batch, _side_q = 1, []
+        side_submit, flush_side = FlatParamStore.side_submit, FlatParamStore.flush_side
 
         def side_stream(self):
             return self._side
@@ -85,6 +93,7 @@ def test_layernorm_side_fold_only_into_main_grad_views(frozen_bias, monkeypatch)
 
     class _Hooks:
         store = _Store()
+        store.hooks = None  # set below: flush_side marks readiness through the store's hooks
 
         def accumulate_for(self, p):
             return False
@@ -92,8 +101,10 @@ def test_layernorm_side_fold_only_into_main_grad_views(frozen_bias, monkeypatch)
         def ready(self, p):
             pass
 
+    _Hooks.store.hooks = _Hooks()
     real_launch = kf._side_launch
-    monkeypatch.setattr(kf, "_side_launch", lambda w, launch, *inp: (calls.append(1), real_launch(w, launch, *inp)))
+    monkeypatch.setattr(kf, "_side_launch",
+                        lambda w, launch, *inp, **kw: (calls.append(1), real_launch(w, launch, *inp, **kw)))
     monkeypatch.setattr(kf, "SIDE_LAG_CYCLES", 1_000_000)
     torch.manual_seed(3)
     H, T = 768, 512

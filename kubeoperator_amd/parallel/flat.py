@@ -169,6 +169,7 @@ class FlatParamStore:
         # over 1; 12-64 no better (profiles/r6_gpt2_side_batch_bucket_ab.jsonl, r6_gpt2_side_hint_ab.jsonl)
         self.side_batch = max(1, int(os.environ.get("KOP_SIDE_BATCH", "8")))
         self._side_q: list = []
+        self._flush_at_end = False  # an end-of-backward flush is queued with the autograd engine
         self.gate_waits: list | None = None  # (event, event) around collective-gate waits (exposed comm timing)
         self.wgrad_stream = False  # issue weight gradients on it (set by the trainer)
         name_to_bucket = {nm: b for b in self.buckets for nm in b.names}
@@ -283,8 +284,19 @@ class FlatParamStore:
         ``side_batch``, and by ``flush_side``: every caller flushes before anything that depends on the queued
         launches having been issued (deferred launches, the end of backward, the join)."""
         self._side_q.append((launch, tuple(inputs), tuple(ready)))
+        if not self._flush_at_end:
+            # whatever the caller: the last group goes out when the backward pass that queued it ends
+            try:
+                torch.autograd.Variable._execution_engine.queue_callback(self._end_of_backward)
+                self._flush_at_end = True
+            except RuntimeError:  # not inside a backward pass: the caller flushes
+                pass
         if len(self._side_q) >= self.side_batch:
             self.flush_side()
+
+    def _end_of_backward(self) -> None:
+        self._flush_at_end = False
+        self.flush_side()
 
     def flush_side(self) -> None:
         """Issue the queued side-stream launches behind one fork from the compute stream: the side stream waits for

@@ -44,6 +44,34 @@ def _train(model: str, stream: bool, accum: int, monkeypatch, hold: bool = True,
     return init, tr.store.params.detach().float()
 
 
+_HAZARD = """
+import sys, pytest, torch
+sys.path.insert(0, {root!r})
+from tests.test_wgrad_stream_gpu import _train
+mp = pytest.MonkeyPatch()
+init, off = _train("tiny_llama", False, 1, mp)
+_, on = _train("tiny_llama", True, 1, mp, hold=False)
+print("REL", ((on - off).norm() / (off - init).norm()).item())
+"""
+
+
+def test_lag_without_reference_hold_reproduces_divergence():
+    """Documents the root cause: without ``hold_side`` the in-place residual-gradient accumulation races the
+    lagging side stream and layer 0's Wo gradient is wrong. In a fresh process: HIP maps streams onto the
+    GPU_MAX_HW_QUEUES hardware queues in creation order, and a side stream that shares the compute stream's queue runs
+    in its order and cannot race -- which queue it lands on depends on how many streams the process made before."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", _HAZARD.format(root=root)], capture_output=True, text=True,
+                         timeout=150, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    rel = float(out.stdout.split("REL")[-1])
+    assert rel > 2e-2, rel
+
+
 @pytest.mark.parametrize("model", ["tiny_llama", "tiny_gpt2"])
 @pytest.mark.parametrize("accum", [1, 4])
 @pytest.mark.parametrize("batch", [1, 6])
@@ -54,15 +82,6 @@ def test_lagging_side_stream_matches_one_stream(model, accum, batch, monkeypatch
     _, on = _train(model, True, accum, monkeypatch, batch=batch)
     rel = ((on - off).norm() / (off - init).norm()).item()
     assert rel < 5e-3, rel
-
-
-def test_lag_without_reference_hold_reproduces_divergence(monkeypatch):
-    """Documents the root cause: without ``hold_side`` the in-place residual-gradient accumulation races the
-    lagging side stream and layer 0's Wo gradient is wrong."""
-    init, off = _train("tiny_llama", False, 1, monkeypatch)
-    _, on = _train("tiny_llama", True, 1, monkeypatch, hold=False)
-    rel = ((on - off).norm() / (off - init).norm()).item()
-    assert rel > 2e-2, rel
 
 
 @pytest.mark.parametrize("frozen_bias", [True, False])
@@ -79,8 +98,9 @@ def test_layernorm_side_fold_only_into_main_grad_views(frozen_bias, monkeypatch)
     class _Store:
         wgrad_stream = True
         _side = torch.cuda.Stream()
-        side_batch, _side_q = 1, []
+        side_batch, _side_q, _flush_at_end = 1, [], False
         side_submit, flush_side = FlatParamStore.side_submit, FlatParamStore.flush_side
+        _end_of_backward = FlatParamStore._end_of_backward
 
         def side_stream(self):
             return self._side

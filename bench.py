@@ -22,7 +22,8 @@ reduce-scatter or all-reduce / the ZeRO-1 all-gather per optimizer step) and ``e
 over ranks): the compute stream's stall between backward's last kernel and the completion of the last gradient
 collective, plus its stalls on ZeRO-1 all-gather gates in the next forward -- CUDA-event timed on the GPU.
 ``runtime`` records torch / HIP / RCCL versions and every ``NCCL_*`` / ``RCCL_*`` / ``HSA_*`` / ``TORCH_NCCL_*`` /
-``HIP_*`` variable in effect; ``cpu_affinity_rank0`` the CPUs rank 0 was pinned to (N > 1: each rank is bound to
+``HIP_*`` variable in effect; ``gpu_telemetry_rank0`` the board power and shader clock sampled over the timed
+steps (sysfs, read-only; per rank in ``ranks``); ``cpu_affinity_rank0`` the CPUs rank 0 was pinned to (N > 1: each rank is bound to
 its GPU's NUMA-local CPUs and sizes its thread pool to them, ``parallel/dist.py`` ``bind_rank_cpus``, with the reason
 of any fallback). ``ranks`` (N > 1): one record per rank -- its pinning, its exposed waits (``finish_wait_ms``: the
 compute stream's stall for the last gradient collective; ``gate_wait_ms``: its stalls on ZeRO-1 all-gather gates) and
@@ -173,6 +174,13 @@ def main() -> int:
         # per-bucket timeline (ready events + RCCL's own durations); KOP_BENCH_TIMELINE=0 turns it off (A/B)
         trainer.dp.timeline = [] if os.environ.get("KOP_BENCH_TIMELINE", "1") != "0" else None
     comm0, gather0 = trainer.dp.comm_bytes, trainer.dp.gather_bytes
+    # board power and shader clock of this rank's GPU over the timed steps (sysfs, read-only; the clock the
+    # power cap leaves differs by a few % between boxes: train/gpu_telemetry.py)
+    sampler = None
+    if cuda and os.environ.get("KOP_BENCH_TELEMETRY", "1") != "0":  # 0: no sampler thread (A/B)
+        from kubeoperator_amd.train.gpu_telemetry import PowerClockSampler
+
+        sampler = PowerClockSampler(info.device.index or 0).start()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = trainer.train_step(data.batches(args.accum))
@@ -180,6 +188,7 @@ def main() -> int:
     barrier(info)
     sync()
     elapsed = time.perf_counter() - t0
+    telemetry = sampler.stop() if sampler is not None else None
     elapsed = all_reduce_max(elapsed, info)
     exposed_ms = None
     ranks = None
@@ -193,7 +202,8 @@ def main() -> int:
         # land in rank 0's JSON line, so a slow rank or a late bucket is attributable)
         from kubeoperator_amd.parallel.ddp import timeline_summary
 
-        rec = {"rank": info.rank, "affinity": affinity, "finish_wait_ms": round(fin, 3), "gate_wait_ms": round(gate, 3),
+        rec = {"rank": info.rank, "affinity": affinity, "gpu_telemetry": telemetry,
+               "finish_wait_ms": round(fin, 3), "gate_wait_ms": round(gate, 3),
                "gate_waits_per_step": len(trainer.store.gate_waits) // max(1, args.steps),
                "buckets": timeline_summary(trainer.dp.timeline) if trainer.dp.timeline is not None else None}
         ranks = gather_objects(rec, info)
@@ -256,6 +266,7 @@ def main() -> int:
             "param_gather_bytes_per_step": int(gather_step),
             "exposed_comm_ms": round(exposed_ms, 3) if exposed_ms is not None else None,
             "cpu_affinity_rank0": affinity,
+            "gpu_telemetry_rank0": telemetry,
             "streams": streams,
             "ranks": ranks,
             "runtime": runtime_env(),

@@ -54,3 +54,24 @@ def test_stream_gaps_sums_same_stream_gaps_per_kernel_pair_inside_the_step_windo
     assert set(s0["pairs"]) == {("gemm_a", "gelu_bwd"), ("gelu_bwd", "kop::clip_coef_kernel")}
     assert abs(s0["gap_ms"] - (12 + 11 + 31) / 2 / 1e3) < 1e-12
     assert res["1"]["gap_ms"] == 0.0
+
+
+def test_gpu_telemetry_parses_sysfs_and_summarizes(tmp_path):
+    from kubeoperator_amd.train import gpu_telemetry as gt
+
+    assert gt.parse_sclk("0: 500Mhz\n1: 1650Mhz\n2: 2400Mhz *\n") == 2400
+    assert gt.parse_sclk("0: 500Mhz\n1: 1918Mhz *\n2: 2400Mhz\n") == 1918
+    assert gt.parse_sclk("0: 500Mhz\n") is None
+    dev, hw = tmp_path / "dev", tmp_path / "dev" / "hwmon" / "hwmon3"
+    hw.mkdir(parents=True)
+    (dev / "pp_dpm_sclk").write_text("0: 500Mhz\n1: 1900Mhz *\n")
+    (hw / "power1_average").write_text("1312000000\n")
+    s = gt.PowerClockSampler(where=(str(dev), str(hw)))
+    t, p, c = s.read()
+    assert (p, c) == (1312.0, 1900)
+    s.samples = [(0, 1300.0, 1900), (1, 1320.0, None), (2, None, 1920)]
+    s.where = (str(dev), str(hw))
+    r = s.stop()
+    assert r["power_w"] == {"n": 2, "mean": 1310.0, "min": 1300.0, "max": 1320.0}
+    assert r["sclk_mhz"]["n"] == 2 and r["sclk_mhz"]["max"] == 1920
+    assert gt.PowerClockSampler(where=()).start().stop() is None  # no sysfs: no thread, no record

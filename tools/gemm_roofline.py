@@ -15,12 +15,10 @@ Prints one JSON line per signature (largest in-step time first) and a final summ
 from __future__ import annotations
 
 import argparse
-import glob
 import json
 import os
 import statistics
 import sys
-import threading
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -95,67 +93,21 @@ class Recorder(TorchDispatchMode):
         return out
 
 
-def _hwmon_dir():
-    from kubeoperator_amd.parallel.dist import _gpu_pci_dir
-
-    try:
-        d = _gpu_pci_dir(torch.cuda.current_device())
-    except Exception:  # noqa: BLE001
-        return None
-    hw = sorted(glob.glob(d + "/hwmon/hwmon*"))
-    return (d, hw[0] if hw else None)
-
-
 class Sampler:
-    """Board power (W) and current shader clock (MHz) of this GPU from sysfs, every ``period`` s (read-only)."""
+    """Board power (W) and current shader clock (MHz) of this GPU (train/gpu_telemetry.py), every ``period`` s."""
 
     def __init__(self, period=0.05):
-        self.period = period
-        self.where = _hwmon_dir()
-        self.samples = []
-        self._stop = threading.Event()
-        self.t = None
+        from kubeoperator_amd.train.gpu_telemetry import PowerClockSampler
 
-    def _read(self):
-        if not self.where:
-            return None
-        dev, hw = self.where
-        p = c = None
-        for f in ("power1_average", "power1_input"):
-            try:
-                p = int(open(f"{hw}/{f}").read()) / 1e6
-                break
-            except (OSError, TypeError, ValueError):
-                continue
-        try:
-            for line in open(f"{dev}/pp_dpm_sclk"):
-                if line.strip().endswith("*"):
-                    c = int(line.split(":")[1].strip().split("Mhz")[0].split("MHz")[0])
-        except (OSError, ValueError, IndexError):
-            pass
-        return (time.time(), p, c)
-
-    def _loop(self):
-        while not self._stop.is_set():
-            r = self._read()
-            if r:
-                self.samples.append(r)
-            time.sleep(self.period)
+        self._s = PowerClockSampler(torch.cuda.current_device(), period)
 
     def start(self):
-        self.samples, self._stop = [], threading.Event()
-        self.t = threading.Thread(target=self._loop, daemon=True)
-        self.t.start()
+        self._s.start()
         return self
 
     def stop(self):
-        self._stop.set()
-        if self.t:
-            self.t.join()
-        p = [s[1] for s in self.samples if s[1] is not None]
-        c = [s[2] for s in self.samples if s[2] is not None]
-        f = lambda xs: {"n": len(xs), "mean": round(statistics.mean(xs), 1), "min": min(xs), "max": max(xs)} if xs else None  # noqa: E731
-        return {"power_w": f(p), "sclk_mhz": f(c)}
+        r = self._s.stop() or {}
+        return {"power_w": r.get("power_w"), "sclk_mhz": r.get("sclk_mhz")}
 
 
 def isolated(sig, iters=20):

@@ -180,7 +180,7 @@ def main() -> int:
     if cuda and os.environ.get("KOP_BENCH_TELEMETRY", "1") != "0":  # 0: no sampler thread (A/B)
         from kubeoperator_amd.train.gpu_telemetry import PowerClockSampler
 
-        sampler = PowerClockSampler(info.device.index or 0).start()
+        sampler = PowerClockSampler(info.device.index or 0, period=0.5).start()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = trainer.train_step(data.batches(args.accum))

@@ -3,8 +3,9 @@
 MI355X boards hold their power cap through a training step (~1.3-1.4 kW) and trade shader clock for it: the
 library GEMMs of the Llama-3-8B step ran at ~1.9 GHz of the 2.4 GHz maximum (``profiles/r4_gemm_roofline.md``), and
 boxes of the pool differ by a few percent in the clock they hold -- the same code measures a few percent apart on
-two boxes. ``bench.py`` samples both every 100 ms over the timed steps and reports them next to the tokens/s, so a
-number can be read against the clock it was measured at.
+two boxes. ``bench.py`` samples both every 0.5 s over the timed steps and reports them next to the tokens/s, so a
+number can be read against the clock it was measured at (sampling every 0.1 s cost the Llama-3-8B step ~0.25 %,
+``profiles/r6_bench_telemetry_ab.jsonl``).
 
 Sources: ``/sys/bus/pci/devices/<gpu>/hwmon/hwmon*/power1_average`` (µW; ``power1_input`` where the average is
 absent) and ``pp_dpm_sclk`` (the DPM level marked ``*`` is the current clock). Nothing is written.

@@ -457,3 +457,67 @@ def test_serving_chart_flags_exist_in_the_server_cli():
     assert {"--model", "--max-batch", "--fp8", "--ckpt"} <= flags
     src = open(server.__file__).read()
     assert not [f for f in flags if f'"{f}"' not in src]
+
+
+def test_side_stream_groups_issue_in_order_and_mark_ready_after_their_launches(monkeypatch):
+    """FlatParamStore.side_submit / flush_side with the CUDA stream calls stubbed out: launches go out in groups of
+    ``side_batch`` behind ONE fork each, in submission order, every parameter is marked ready only after its group
+    was issued, and the group still queued when a backward pass ends is flushed by the autograd engine's final
+    callback (no caller has to flush)."""
+    from kubeoperator_amd.parallel.flat import FlatParamStore
+
+    log = []
+
+    class _Side:
+        def wait_stream(self, s):
+            log.append("fork")
+
+    class _Ctx:
+        def __enter__(self):
+            return self
+
+        def __exit__(self, *a):
+            return False
+
+    monkeypatch.setattr(torch.cuda, "current_stream", lambda *a: None)
+    monkeypatch.setattr(torch.cuda, "stream", lambda s: _Ctx())
+    monkeypatch.setattr(torch.Tensor, "record_stream", lambda self, s: None, raising=False)
+
+    class _Hooks:
+        def ready(self, p):
+            log.append(f"ready:{p}")
+
+    class _Store:
+        side_batch, _side_q, _flush_at_end = 3, [], False
+        hooks = _Hooks()
+        side_submit, flush_side = FlatParamStore.side_submit, FlatParamStore.flush_side
+        _end_of_backward = FlatParamStore._end_of_backward
+
+        def side_stream(self):
+            return _Side()
+
+        def hold_side(self, ins):
+            log.append(f"hold:{len(ins)}")
+
+    st = _Store()
+    t = torch.zeros(2)
+
+    class _F(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x):
+            return x * 1
+
+        @staticmethod
+        def backward(ctx, g):
+            for i in range(5):
+                st.side_submit(lambda i=i: log.append(f"launch:{i}"), (t,), (f"p{i}",))
+            return g
+
+    x = torch.ones(2, requires_grad=True)
+    _F.apply(x).sum().backward()
+    assert log == ["fork", "launch:0", "launch:1", "launch:2", "hold:3", "ready:p0", "ready:p1", "ready:p2",
+                   "fork", "launch:3", "launch:4", "hold:2", "ready:p3", "ready:p4"]
+    assert st._side_q == [] and st._flush_at_end is False
+    log.clear()
+    st.flush_side()  # nothing queued: no fork
+    assert log == []

@@ -219,6 +219,7 @@ def main() -> int:
     cfg = trainer.cfg
     flops_tok = cfg.flops_per_token(args.seq)
     mem_gb = torch.cuda.max_memory_allocated() / 1e9 if cuda else 0.0
+    reserved_gb = torch.cuda.max_memory_reserved() / 1e9 if cuda else 0.0
     if info.is_main:
         model_name = {"llama3_8b": "Llama-3-8B", "gpt2_small": "GPT-2-small",
                       "llama3_70b": "Llama-3-70B"}.get(args.model, args.model)
@@ -258,6 +259,7 @@ def main() -> int:
             "tflops_per_gpu": round(flops_tok * value / world / 1e12, 1),
             "last_loss": round(last_loss, 4),
             "peak_mem_gb_rank0": round(mem_gb, 1),
+            "peak_reserved_gb_rank0": round(reserved_gb, 1),
             "setup_s": round(trainer.setup_seconds, 1),
             "gemm_selection": tuning,
             "backend": info.backend,

@@ -36,8 +36,9 @@ def _lib():
 # Issued on the store's side stream, they run beside the next layer's kernels instead of between them.
 # ``inputs`` are the tensors ``produce`` reads. Two hazards follow from reading them on another stream:
 #
-# * memory reuse: recorded on the side stream (``record_stream``) so the caching allocator does not hand their
-#   memory out before the side stream has run;
+# * memory reuse: the store keeps a reference to every input until the side stream has passed the launch that reads
+#   it (``FlatParamStore.hold_side``), so the caching allocator cannot hand the memory out earlier (no
+#   ``record_stream``: it would hold each block until the side stream's whole queue at free time has run);
 # * in-place accumulation by autograd: when a gradient tensor reaches a node that already holds another
 #   contribution for the same input, autograd adds the two IN PLACE into whichever buffer it holds the last
 #   reference to (``InputBuffer::accumulate``, ``can_accumulate_inplace``). The residual stream makes that
@@ -45,8 +46,7 @@ def _lib():
 #   ``x`` gets two gradients -- the second norm's (which is also the ``dY`` of the Wo / proj projection) and the
 #   first norm's. With the side stream lagging, ``dY += dX1`` ran on the compute stream before the side stream's
 #   dW_o read ``dY``, so Wo of layer 0 received the gradient of dY + dX1 (the round-2 divergence: rel. error 0.29,
-#   identical across runs). The store keeps a reference to every input until the side stream has passed it
-#   (``FlatParamStore.hold_side``), which makes autograd allocate a fresh sum instead of writing into it.
+#   identical across runs). The same references make autograd allocate a fresh sum instead of writing into it.
 #
 # Measured on one MI355X (profiles/r2_wgrad_stream_ab.log): GPT-2-small +8 % (its 768-wide GEMMs leave the chip
 # partly idle), Llama-3-8B -30..-50 % (two full-chip stream-K GEMMs contend), so the trainer enables it per
@@ -110,8 +110,6 @@ def _sink(w: torch.Tensor, produce, *inputs, defer: bool = False):
                 if SIDE_LAG_CYCLES > 0:
                     torch.cuda._sleep(SIDE_LAG_CYCLES)
                 produce(mg, acc)
-            for t in inputs:
-                t.record_stream(side)
             store.hold_side(inputs)
 
         store.defer(launch)

@@ -98,6 +98,15 @@ class GradHooks:
         self.store._param_written(p)
 
 
+# ``record_stream`` on the side stream's inputs as well as ``hold_side``'s references (KOP_SIDE_RECORD_STREAM=1, the
+# round-2..5 behaviour): redundant -- the reference is dropped only after the side stream has passed the reading
+# launch -- and harmful: a block freed with a recorded stream waits for that stream's work queued AT FREE TIME, and the
+# lagging side stream always has some, so the compute stream kept allocating fresh segments. GPT-2-small reserved
+# 245 GB for 57 GB allocated at micro-batch 32 and ran out of memory (then every step synchronised and freed the
+# cache: 4x slower) at micro-batch 64 (profiles/r6_gpt2_side_memory_ab.jsonl)
+_RECORD_STREAM = os.environ.get("KOP_SIDE_RECORD_STREAM", "0") == "1"
+
+
 class FlatParamStore:
     def __init__(self, module: nn.Module, specs: list[ParamSpec], device, dtype=torch.bfloat16, world: int = 1,
                  bucket_bytes: int = 512 * 1024 * 1024, grad_dtype=None):
@@ -269,8 +278,10 @@ class FlatParamStore:
 
     def hold_side(self, tensors) -> None:
         """Keep references to tensors the side stream reads until it has passed them (see ops.functional._sink:
-        a tensor autograd holds the only reference to may be accumulated into IN PLACE on the compute stream).
-        Entries whose event has completed are dropped on the way (host-side query, no synchronisation)."""
+        a tensor autograd holds the only reference to may be accumulated into IN PLACE on the compute stream, and
+        memory the allocator may not hand out again before the side stream has read it). Entries whose event has
+        completed are dropped on the way (host-side query, no synchronisation); ``join_side`` drops the rest once
+        the compute stream is ordered after the side stream."""
         ev = torch.cuda.Event()
         ev.record(self._side)
         held = self._held
@@ -313,8 +324,9 @@ class FlatParamStore:
             for launch, _, _ in q:
                 launch()
         ins = [t for _, inputs, _ in q for t in inputs]
-        for t in ins:
-            t.record_stream(side)
+        if _RECORD_STREAM:
+            for t in ins:
+                t.record_stream(side)
         self.hold_side(ins)
         for _, _, ready in q:
             for p in ready:

@@ -69,7 +69,9 @@ def test_lag_without_reference_hold_reproduces_divergence():
                          timeout=150, cwd=root)
     assert out.returncode == 0, out.stderr[-2000:]
     rel = float(out.stdout.split("REL")[-1])
-    assert rel > 2e-2, rel
+    # nan counts too: with no reference held (and no record_stream) the allocator also reuses inputs' memory under
+    # the lagging side stream
+    assert rel != rel or rel > 2e-2, rel
 
 
 @pytest.mark.parametrize("model", ["tiny_llama", "tiny_gpt2"])

@@ -29,7 +29,7 @@ source "$(dirname "$0")/gpu_lib.sh"
 mkdir -p gpurun_out/prof gpurun_out/pmc
 
 L8B="${L8B:-python bench.py --steps 10 --warmup 3}"
-G2="python bench.py --model gpt2_small --seq 1024 --mbs 32 --steps 20 --warmup 5"
+G2="python bench.py --model gpt2_small --seq 1024 --mbs 64 --accum 2 --steps 20 --warmup 5"
 port=29700
 
 torchrun_n() {  # name limit nproc args...
@@ -68,7 +68,7 @@ s_prof_l8b() {
 }
 s_prof_gpt2() {
   step prof_gpt2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/gpt2 -o gpt2 --output-format csv -- \
-    python3 bench.py --model gpt2_small --seq 1024 --mbs 32 --steps 3 --warmup 2
+    python3 bench.py --model gpt2_small --seq 1024 --mbs 64 --accum 2 --steps 3 --warmup 2
 }
 
 s_pmc_attn() {

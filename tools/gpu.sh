@@ -64,7 +64,7 @@ s_check() { s_tests && s_smoke && step bench 400 $L8B && step gpt2 300 $G2; }
 
 s_prof_l8b() {
   step prof_l8b 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/l8b -o l8b --output-format csv -- \
-    python3 bench.py --steps 2 --warmup 1
+    python3 bench.py --steps 3 --warmup 1
 }
 s_prof_gpt2() {
   step prof_gpt2 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/gpt2 -o gpt2 --output-format csv -- \

@@ -57,7 +57,10 @@ def _lib():
 SIDE_LAG_CYCLES = int(os.environ.get("KOP_SIDE_LAG_CYCLES", "0"))
 
 
-_NORM_SIDE = os.environ.get("KOP_NORM_SIDE", "1") != "0"  # norm weight-gradient folds on the side stream (A/B: 0)
+# norm weight / bias gradient folds on the side stream (KOP_NORM_SIDE=1). Round 5 kept them there (+0.7 % on GPT-2-small);
+# with the grouped side launches, no record_stream and the 64 x 2 shape they are cheaper inside the norm backward:
+# off +0.2..1.3 % over five same-box alternations (profiles/r6_gpt2_norm_side_ab_1.jsonl, _2.jsonl)
+_NORM_SIDE = os.environ.get("KOP_NORM_SIDE", "0") == "1"
 
 
 def _side_active(w) -> bool:

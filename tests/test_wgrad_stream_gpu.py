@@ -14,7 +14,8 @@ pytestmark = pytest.mark.gpu
 LAG = 1_000_000  # GPU clock cycles per weight gradient
 
 
-def _train(model: str, stream: bool, accum: int, monkeypatch, hold: bool = True, batch: int = 1):
+def _train(model: str, stream: bool, accum: int, monkeypatch, hold: bool = True, batch: int = 1,
+           norm_side: bool = False):
     from kubeoperator_amd.ops import functional
     from kubeoperator_amd.parallel.dist import DistInfo
     from kubeoperator_amd.parallel.flat import FlatParamStore
@@ -23,6 +24,7 @@ def _train(model: str, stream: bool, accum: int, monkeypatch, hold: bool = True,
     monkeypatch.setenv("KOP_WGRAD_STREAM", "1" if stream else "0")
     monkeypatch.setenv("KOP_SIDE_BATCH", str(batch))
     monkeypatch.setattr(functional, "SIDE_LAG_CYCLES", LAG if stream else 0)
+    monkeypatch.setattr(functional, "_NORM_SIDE", norm_side)
     if not hold:
         monkeypatch.setattr(FlatParamStore, "hold_side", lambda self, tensors: None)
     # clipping off: the grad-norm sum uses float atomics, the rest of the step is deterministic
@@ -81,7 +83,7 @@ def test_lagging_side_stream_matches_one_stream(model, accum, batch, monkeypatch
     """``batch``: side-stream launches grouped behind one fork (FlatParamStore.side_submit), the readiness marks and
     the inputs' reference holds following the group."""
     init, off = _train(model, False, accum, monkeypatch)
-    _, on = _train(model, True, accum, monkeypatch, batch=batch)
+    _, on = _train(model, True, accum, monkeypatch, batch=batch, norm_side=batch > 1)  # both norm-fold placements
     rel = ((on - off).norm() / (off - init).norm()).item()
     assert rel < 5e-3, rel
 
@@ -128,6 +130,7 @@ def test_layernorm_side_fold_only_into_main_grad_views(frozen_bias, monkeypatch)
     monkeypatch.setattr(kf, "_side_launch",
                         lambda w, launch, *inp, **kw: (calls.append(1), real_launch(w, launch, *inp, **kw)))
     monkeypatch.setattr(kf, "SIDE_LAG_CYCLES", 1_000_000)
+    monkeypatch.setattr(kf, "_NORM_SIDE", True)  # the fold's side-stream path (opt-in since round 6)
     torch.manual_seed(3)
     H, T = 768, 512
     x = torch.randn(T, H, device="cuda", dtype=torch.bfloat16, requires_grad=True)
